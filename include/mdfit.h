@@ -1,0 +1,173 @@
+/*
+ * mdfit.h — C-ABI of the MI355X-native per-TaxID ancient-DNA damage-fit engine.
+ *
+ * This is the drop-in boundary for the hot path of metadamage's fits.py
+ * (reference: /root/reference/metadamage/fits.py).  The reference has no FFI;
+ * its operator boundary is the per-taxon numpyro call chain
+ *
+ *     fit_single_group_without_timeout(group, cfg, ...)   fits.py:428-469
+ *       group_to_numpyro_data                              fits.py:398-419
+ *       fit_mcmc(mcmc_PMD / mcmc_null, data)               fits.py:382-387, 438-439
+ *       compute_fit_results                                fits.py:230-295
+ *         add_assymetry_results_to_fit_results             fits.py:298-356
+ *         add_noise_estimates                              fits.py:359-376
+ *
+ * dispatched by compute_fits (fits.py:709-730).  mdfit_fit_batch replaces the
+ * whole chain for a batch of taxa in one stream-ordered launch: one call per
+ * device, outputs in input order (so the reference's reorder step,
+ * fits.py:422-425, is a no-op).
+ *
+ * Conventions
+ *  - Every pointer argument of mdfit_fit_batch is a DEVICE pointer (HBM); the
+ *    caller owns all buffers (PyTorch tensors in the Python host).  The library
+ *    allocates no persistent device memory.
+ *  - The call is asynchronous on `hip_stream` (a hipStream_t, NULL = default
+ *    stream) and never synchronises the host.
+ *  - Return value: 0 on success, otherwise a negative MDFIT_E* code or a
+ *    positive hipError_t; mdfit_last_error() gives a message (thread-local).
+ *  - Per-taxon failures are reported in status[] and never abort the batch.
+ */
+#ifndef MDFIT_H
+#define MDFIT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MDFIT_ABI_VERSION 1
+
+/* Dense count layout: one row of MDFIT_LD uint32 per taxon.
+ * Column i < 15 is forward position z = i+1 (y = CT, N = C by default);
+ * column 15 <= i < 30 is reverse position z = -(i-14) (y = GA, N = G).
+ * Columns 30, 31 are padding (ignored).  This is group_to_numpyro_data
+ * (fits.py:398-419) packed for a whole batch. */
+#define MDFIT_NPOS 30
+#define MDFIT_NHALF 15
+#define MDFIT_LD 32
+
+/* Mismatch counts for the noise estimate (fits.py:359-376): uint32
+ * mm[T][30][12], columns in the reference order AC AG AT CA CG CT GA GC GT TA TC TG. */
+#define MDFIT_NMM 12
+
+/* Fit modes. */
+#define MDFIT_MODE_MAP 0  /* maximum a posteriori of model_PMD / model_null (fits.py:43-67) */
+
+/* Per-taxon status codes (status[t]). */
+#define MDFIT_OK 0
+#define MDFIT_MAXITER 1   /* a sub-fit hit max_iter before converging */
+#define MDFIT_NONFINITE 2 /* non-finite objective at the returned point */
+#define MDFIT_INVALID 3   /* invalid input (y > N somewhere) */
+
+/* Error codes (return values). */
+#define MDFIT_E_ARG (-1)
+#define MDFIT_E_HIP (-2)
+
+/* Output record: double out[T][MDFIT_NOUT].  Fields 0..24 are the numeric
+ * columns of fit_results (fits.py:244-293, 317-356, 374-376) in the reference
+ * column order; the rest are per-sub-fit diagnostics. */
+enum mdfit_field {
+  MDFIT_F_D_MAX = 0,
+  MDFIT_F_N_SIGMA,
+  MDFIT_F_D_MAX_LOWER_HPDI,
+  MDFIT_F_D_MAX_UPPER_HPDI,
+  MDFIT_F_Q_MEAN,
+  MDFIT_F_CONCENTRATION_MEAN,
+  MDFIT_F_D_MAX_MARGINALIZED_MEAN,
+  MDFIT_F_N_Z1_FORWARD,
+  MDFIT_F_N_Z1_REVERSE,
+  MDFIT_F_N_SUM_FORWARD,
+  MDFIT_F_N_SUM_REVERSE,
+  MDFIT_F_N_SUM_TOTAL,
+  MDFIT_F_Y_SUM_FORWARD,
+  MDFIT_F_Y_SUM_REVERSE,
+  MDFIT_F_Y_SUM_TOTAL,
+  MDFIT_F_N_SIGMA_FORWARD,
+  MDFIT_F_D_MAX_FORWARD,
+  MDFIT_F_Q_MEAN_FORWARD,
+  MDFIT_F_N_SIGMA_REVERSE,
+  MDFIT_F_D_MAX_REVERSE,
+  MDFIT_F_Q_MEAN_REVERSE,
+  MDFIT_F_ASYMMETRY,
+  MDFIT_F_NORMALIZED_NOISE,
+  MDFIT_F_NORMALIZED_NOISE_FORWARD,
+  MDFIT_F_NORMALIZED_NOISE_REVERSE,
+  MDFIT_NRESULT, /* = 25 result columns */
+  /* diagnostics: sub-fit k in {0 PMD-all, 1 null-all, 2 PMD-fwd, 3 PMD-rev,
+   * 4 null-fwd, 5 null-rev} occupies MDFIT_F_DIAG + 8*k + {q, A, c, phi,
+   * objective, evaluations, status, unused}.  Null sub-fits store A = c = 0. */
+  MDFIT_F_DIAG = 32,
+  MDFIT_NOUT = 80
+};
+
+#define MDFIT_NSUBFIT 6
+#define MDFIT_DIAG_STRIDE 8
+
+/* Prediction record: float pred[T][3][30] = (median, hdpi_lower, hdpi_upper)
+ * per position, the payload of fit_predictions (fits.py:632-665). */
+#define MDFIT_NPRED 3
+
+typedef struct mdfit_opts {
+  int32_t mode;       /* MDFIT_MODE_MAP */
+  int32_t max_iter;   /* objective evaluations per sub-fit (default 200) */
+  double tol_step;    /* convergence: max |Newton step| in unconstrained units (default 1e-9) */
+  uint64_t seed;      /* reserved for the sampling mode */
+  int32_t num_warmup; /* reserved for the sampling mode */
+  int32_t num_samples;/* reserved for the sampling mode */
+} mdfit_opts;
+
+/* Fill `opts` with defaults. */
+void mdfit_default_opts(mdfit_opts* opts);
+
+/*
+ * Fit a batch of taxa.
+ *   y, N      : const uint32_t[n_taxa][MDFIT_LD]           (device)
+ *   mm        : const uint32_t[n_taxa][30][MDFIT_NMM] or NULL (device; NULL -> noise columns NaN)
+ *   out       : double[n_taxa][MDFIT_NOUT]                  (device)
+ *   pred      : float[n_taxa][MDFIT_NPRED][MDFIT_NPOS] or NULL (device)
+ *   status    : int32_t[n_taxa]                             (device)
+ *   workspace : device buffer of mdfit_workspace_bytes() bytes (work-queue counter)
+ *   hip_stream: hipStream_t or NULL
+ * Replaces compute_fits' per-taxon loop (fits.py:477-526, 569-626, 709-730).
+ */
+int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm,
+                    int64_t n_taxa, const mdfit_opts* opts, double* out,
+                    float* pred, int32_t* status, void* workspace,
+                    void* hip_stream);
+
+/* Bytes of device workspace mdfit_fit_batch needs. */
+int64_t mdfit_workspace_bytes(void);
+
+/*
+ * Pointwise beta-binomial log-pmf (numpyro BetaBinomial.log_prob, used by
+ * fits.py:59,67 and log_likelihood fits.py:126-133):
+ *   out[i] = log C(N,y) + lnB(y+alpha, N-y+beta) - lnB(alpha, beta)
+ * plus d/dalpha, d/dbeta (grad[i][2]).  Device pointers; for parity tests.
+ */
+int mdfit_betabinom_logpmf(const double* y, const double* N, const double* alpha,
+                           const double* beta, int64_t n, double* out,
+                           double* grad, void* hip_stream);
+
+/*
+ * Device special functions on an array (parity tests): out[i] =
+ * (lgamma(x), digamma(x), trigamma(x)) for x[i] > 0.  Device pointers.
+ */
+int mdfit_special(const double* x, int64_t n, double* out3, void* hip_stream);
+
+/*
+ * Register-only throughput probe of the per-point evaluation the fit kernel
+ * runs (value + gradient + Hessian of one beta-binomial point): launches
+ * `n_waves` waves that each do `iters` evaluations; `sink` is a device
+ * double[n_waves*64].  Used by bench.py for the compute roofline.
+ */
+int mdfit_peak_probe(int64_t n_waves, int32_t iters, double* sink, void* hip_stream);
+
+const char* mdfit_last_error(void);
+int mdfit_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MDFIT_H */

@@ -1,0 +1,143 @@
+"""Device-side entry points: PyTorch-ROCm tensors in, C-ABI call, tensors out.
+
+PyTorch only provides device memory and the stream; every computation runs in
+the HIP kernels of libmdfit.so (metadamage_amd/csrc/mdfit.hip).  There is no
+CPU fallback: without a GPU these functions raise.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+
+
+def _torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        raise _lib.MdfitError("no HIP device available: the mdfit engine runs on MI355X only")
+    return torch
+
+
+def _stream_handle(torch, stream=None) -> ctypes.c_void_p:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+@dataclass
+class FitBatch:
+    """Device-resident results of one mdfit_fit_batch call."""
+
+    out: "object"  # torch.float64 [T, NOUT]
+    pred: "object"  # torch.float32 [T, 3, 30]
+    status: "object"  # torch.int32 [T]
+
+
+def to_device_counts(y, N, mm=None, device="cuda"):
+    """Host uint32 arrays -> device tensors in the engine's dense layout."""
+    torch = _torch()
+    y = np.ascontiguousarray(y, dtype=np.uint32)
+    N = np.ascontiguousarray(N, dtype=np.uint32)
+    if y.ndim != 2 or y.shape[1] != _lib.LD or N.shape != y.shape:
+        raise ValueError(f"y, N must be uint32[T][{_lib.LD}], got {y.shape} / {N.shape}")
+    ty = torch.from_numpy(y.view(np.int32)).to(device)
+    tN = torch.from_numpy(N.view(np.int32)).to(device)
+    tm = None
+    if mm is not None:
+        mm = np.ascontiguousarray(mm, dtype=np.uint32)
+        if mm.shape != (y.shape[0], _lib.NPOS, _lib.NMM):
+            raise ValueError(f"mm must be uint32[T][30][12], got {mm.shape}")
+        tm = torch.from_numpy(mm.view(np.int32)).to(device)
+    return ty, tN, tm
+
+
+def alloc_outputs(n_taxa: int, device="cuda", with_pred: bool = True) -> FitBatch:
+    torch = _torch()
+    out = torch.empty((n_taxa, _lib.NOUT), dtype=torch.float64, device=device)
+    pred = (
+        torch.empty((n_taxa, _lib.NPRED, _lib.NPOS), dtype=torch.float32, device=device)
+        if with_pred
+        else None
+    )
+    status = torch.empty((n_taxa,), dtype=torch.int32, device=device)
+    return FitBatch(out, pred, status)
+
+
+def fit_batch_device(ty, tN, tm=None, opts: _lib.MdfitOpts | None = None, res: FitBatch | None = None,
+                     stream=None) -> FitBatch:
+    """Launch mdfit_fit_batch on device tensors (asynchronous on `stream`)."""
+    torch = _torch()
+    lib = _lib.load()
+    T = int(ty.shape[0])
+    for name, t in (("y", ty), ("N", tN)):
+        if not (t.is_cuda and t.is_contiguous() and t.dtype == torch.int32 and tuple(t.shape) == (T, _lib.LD)):
+            raise ValueError(f"{name} must be a contiguous cuda int32/uint32 view of shape [T, {_lib.LD}]")
+    if tm is not None and not (tm.is_cuda and tm.is_contiguous() and tm.numel() == T * _lib.NPOS * _lib.NMM):
+        raise ValueError("mm must be a contiguous cuda tensor of T*30*12 uint32")
+    if res is None:
+        res = alloc_outputs(T, device=ty.device)
+    o = opts if opts is not None else _lib.default_opts()
+    _lib.check(
+        lib.mdfit_fit_batch(
+            ctypes.c_void_p(ty.data_ptr()),
+            ctypes.c_void_p(tN.data_ptr()),
+            ctypes.c_void_p(tm.data_ptr()) if tm is not None else None,
+            T,
+            ctypes.byref(o),
+            ctypes.c_void_p(res.out.data_ptr()),
+            ctypes.c_void_p(res.pred.data_ptr()) if res.pred is not None else None,
+            ctypes.c_void_p(res.status.data_ptr()),
+            None,
+            _stream_handle(torch, stream),
+        )
+    )
+    return res
+
+
+def fit_batch(y, N, mm=None, opts: _lib.MdfitOpts | None = None, device="cuda"):
+    """Host arrays in, host arrays out: (out[T,80] f64, pred[T,3,30] f32, status[T] i32)."""
+    torch = _torch()
+    ty, tN, tm = to_device_counts(y, N, mm, device=device)
+    res = fit_batch_device(ty, tN, tm, opts)
+    torch.cuda.current_stream().synchronize()
+    return res.out.cpu().numpy(), res.pred.cpu().numpy(), res.status.cpu().numpy()
+
+
+def special(x, device="cuda"):
+    """(lgamma, digamma, trigamma) of x on the device (parity tests)."""
+    torch = _torch()
+    lib = _lib.load()
+    tx = torch.as_tensor(np.ascontiguousarray(x, dtype=np.float64), device=device)
+    o = torch.empty((tx.numel(), 3), dtype=torch.float64, device=device)
+    _lib.check(lib.mdfit_special(ctypes.c_void_p(tx.data_ptr()), tx.numel(), ctypes.c_void_p(o.data_ptr()),
+                                 _stream_handle(torch)))
+    torch.cuda.current_stream().synchronize()
+    return o.cpu().numpy()
+
+
+def betabinom_logpmf(y, N, a, b, device="cuda"):
+    """Pointwise beta-binomial log-pmf and (d/dalpha, d/dbeta) on the device."""
+    torch = _torch()
+    lib = _lib.load()
+    ts = [torch.as_tensor(np.ascontiguousarray(v, dtype=np.float64), device=device) for v in (y, N, a, b)]
+    n = ts[0].numel()
+    o = torch.empty(n, dtype=torch.float64, device=device)
+    g = torch.empty((n, 2), dtype=torch.float64, device=device)
+    _lib.check(lib.mdfit_betabinom_logpmf(*[ctypes.c_void_p(t.data_ptr()) for t in ts], n,
+                                          ctypes.c_void_p(o.data_ptr()), ctypes.c_void_p(g.data_ptr()),
+                                          _stream_handle(torch)))
+    torch.cuda.current_stream().synchronize()
+    return o.cpu().numpy(), g.cpu().numpy()
+
+
+def peak_probe(n_waves: int, iters: int, stream=None):
+    """Launch the register-only point-evaluation probe; returns the sink tensor."""
+    torch = _torch()
+    lib = _lib.load()
+    sink = torch.empty(n_waves * 64, dtype=torch.float64, device="cuda")
+    _lib.check(lib.mdfit_peak_probe(n_waves, iters, ctypes.c_void_p(sink.data_ptr()), _stream_handle(torch, stream)))
+    return sink

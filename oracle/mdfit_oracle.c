@@ -1,0 +1,657 @@
+/*
+ * mdfit_oracle.c — CPU ORACLE (test infrastructure only).
+ *
+ * Plain-C FP64 restatement of the per-taxon damage fit that the HIP kernel in
+ * metadamage_amd/csrc/mdfit.hip implements.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load this library; the product path never
+ * does.  It is written independently of the kernel (scalar loops over points,
+ * libm lgamma, textbook digamma/trigamma) so that a kernel bug cannot hide in
+ * shared code.
+ *
+ * What it restates (reference = /root/reference/metadamage):
+ *   model_PMD                    fits.py:43-59   (priors, D(z), BetaBinomial)
+ *   model_null                   fits.py:62-67
+ *   BetaBinomial log-pmf         numpyro ^0.4.1 (pyproject.toml:17), same
+ *                                formula as scipy.stats.betabinom.logpmf
+ *   group_to_numpyro_data        fits.py:398-419 (dense [30] layout, z implicit)
+ *   get_lppd_and_waic            fits.py:147-172 (one "sample" = the mode)
+ *   compute_n_sigma              fits.py:194-201
+ *   compute_assymmetry_...       fits.py:204-227
+ *   compute_fit_results          fits.py:230-295 (record assembly)
+ *   add_assymetry_results_...    fits.py:298-356 (fwd/rev sub-fits; the
+ *                                D_max_reverse-on-data_forward quirk, :343-348)
+ *   add_noise_estimates          fits.py:359-376
+ *
+ * The inference is the build-defined MAP mode "MDFIT-MAP v1" (DESIGN.md §3):
+ * the reference only samples with NUTS (fits.py:382-387), so the MAP spec is
+ * ours; parity of the MAP optimum itself is pinned against an independent
+ * scipy optimiser (tests/golden/make_golden_scipy.py), and the WAIC /
+ * n_sigma / asymmetry / noise / packing formulas against the reference's own
+ * functions (tests/golden/make_golden_reference.py).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/mdfit.h"
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define NPOS 30
+#define NHALF 15
+
+/* ---------------------------------------------------------------------------
+ * special functions (oracle versions: libm lgamma, recurrence + asymptotic
+ * series for digamma / trigamma)
+ * ------------------------------------------------------------------------- */
+static double o_lgamma(double x) { return lgamma(x); }
+
+static double o_digamma(double x) {
+  double acc = 0.0;
+  while (x < 12.0) {
+    acc -= 1.0 / x;
+    x += 1.0;
+  }
+  double r = 1.0 / x, r2 = r * r;
+  /* psi(x) ~ ln x - 1/(2x) - sum B_2k / (2k x^2k) */
+  double s = r2 * (1.0 / 12 -
+             r2 * (1.0 / 120 -
+             r2 * (1.0 / 252 -
+             r2 * (1.0 / 240 -
+             r2 * (1.0 / 132 -
+             r2 * (691.0 / 32760 -
+             r2 * (1.0 / 12)))))));
+  return acc + log(x) - 0.5 * r - s;
+}
+
+static double o_trigamma(double x) {
+  double acc = 0.0;
+  while (x < 12.0) {
+    acc += 1.0 / (x * x);
+    x += 1.0;
+  }
+  double r = 1.0 / x, r2 = r * r;
+  /* psi1(x) ~ 1/x + 1/(2x^2) + sum B_2k / x^(2k+1) */
+  double s = r * r2 * (1.0 / 6 -
+             r2 * (1.0 / 30 -
+             r2 * (1.0 / 42 -
+             r2 * (1.0 / 30 -
+             r2 * (5.0 / 66 -
+             r2 * (691.0 / 2730 -
+             r2 * (7.0 / 6)))))));
+  return acc + r + 0.5 * r2 + s;
+}
+
+void oracle_special(const double* x, int64_t n, double* out3) {
+  for (int64_t i = 0; i < n; i++) {
+    out3[3 * i + 0] = o_lgamma(x[i]);
+    out3[3 * i + 1] = o_digamma(x[i]);
+    out3[3 * i + 2] = o_trigamma(x[i]);
+  }
+}
+
+/* numpyro BetaBinomial.log_prob incl. the binomial coefficient */
+void oracle_betabinom_logpmf(const double* y, const double* N, const double* a,
+                             const double* b, int64_t n, double* out,
+                             double* grad) {
+  for (int64_t i = 0; i < n; i++) {
+    double k = y[i], m = N[i];
+    double lc = o_lgamma(m + 1) - o_lgamma(k + 1) - o_lgamma(m - k + 1);
+    double lb1 = o_lgamma(k + a[i]) + o_lgamma(m - k + b[i]) - o_lgamma(m + a[i] + b[i]);
+    double lb0 = o_lgamma(a[i]) + o_lgamma(b[i]) - o_lgamma(a[i] + b[i]);
+    out[i] = lc + lb1 - lb0;
+    if (grad) {
+      double ps = o_digamma(a[i] + b[i]) - o_digamma(m + a[i] + b[i]);
+      grad[2 * i + 0] = o_digamma(k + a[i]) - o_digamma(a[i]) + ps;
+      grad[2 * i + 1] = o_digamma(m - k + b[i]) - o_digamma(b[i]) + ps;
+    }
+  }
+}
+
+/* ---------------------------------------------------------------------------
+ * model pieces
+ * ------------------------------------------------------------------------- */
+enum { M_PMD = 0, M_NULL = 1 };
+enum { P_Q = 0, P_A = 1, P_C = 2, P_D = 3 }; /* u-space parameter slots */
+
+static const double U_LO[4] = {-25.0, -25.0, -25.0, -25.0};
+static const double U_HI[4] = {25.0, 25.0, 25.0, 20.0};
+
+static double softplus(double x) { return (x > 0 ? x : 0.0) + log1p(exp(-fabs(x))); }
+static double sigm(double u) { return 1.0 / (1.0 + exp(-u)); }
+
+typedef struct {
+  double F;        /* objective  -(sum ell_i + log prior)            */
+  double g[4];     /* dF/du                                          */
+  double H[4][4];  /* d2F/du2                                        */
+  double mag;      /* sum |lgamma terms| (noise scale of F)          */
+  double ell[NPOS];/* pointwise log-likelihood (without log C(N,y))  */
+} evalres;
+
+/* absolute position |z| - 1 of dense column i */
+static int kpos(int i) { return i < NHALF ? i : i - NHALF; }
+
+/* Evaluate the objective at u for the points i in [lo, hi). */
+static void evaluate(int model, const uint32_t* y, const uint32_t* N, int lo,
+                     int hi, const double u[4], evalres* r) {
+  double q = sigm(u[P_Q]);
+  double omq = sigm(-u[P_Q]);
+  double l1mq = -softplus(u[P_Q]); /* ln(1-q) */
+  double A = 0, omA = 1, c = 0, omc = 1;
+  if (model == M_PMD) {
+    A = sigm(u[P_A]);
+    omA = sigm(-u[P_A]);
+    c = sigm(u[P_C]);
+    omc = sigm(-u[P_C]);
+  }
+  double delta = exp(u[P_D]);
+  double phi = delta + 2.0;
+
+  double G[4] = {0, 0, 0, 0};
+  double Hh[4][4];
+  memset(Hh, 0, sizeof(Hh));
+  double L = 0.0, mag = 0.0;
+  int infeasible = (model == M_PMD) && (A + c >= 1.0);
+
+  for (int i = lo; i < hi && !infeasible; i++) {
+    int k = kpos(i);
+    double yy = (double)y[i], NN = (double)N[i];
+    double D, Dq = 0, DA = 0, Dc = 0, Dqq = 0, DqA = 0;
+    if (model == M_PMD) {
+      double w = exp(k * l1mq);
+      D = A * w + c;
+      DA = w;
+      Dc = 1.0;
+      if (k >= 1) {
+        double wq = exp((k - 1) * l1mq); /* (1-q)^(k-1) */
+        Dq = -A * k * wq;
+        DqA = -k * wq;
+        if (k >= 2) Dqq = A * k * (k - 1) * exp((k - 2) * l1mq);
+      }
+    } else {
+      D = q;
+      Dq = 1.0;
+    }
+    double omD = 1.0 - D;
+    double a = D * phi, b = omD * phi;
+    double t1 = o_lgamma(yy + a), t2 = o_lgamma(NN - yy + b), t3 = o_lgamma(NN + phi);
+    double t4 = o_lgamma(a), t5 = o_lgamma(b), t6 = o_lgamma(phi);
+    double ell = (t1 - t4) + (t2 - t5) - (t3 - t6); /* exact 0 when N = 0 */
+    mag += fabs(t1) + fabs(t2) + fabs(t3) + fabs(t4) + fabs(t5) + fabs(t6);
+    r->ell[i] = ell;
+    L += ell;
+    double Pa = o_digamma(yy + a) - o_digamma(a);
+    double Pb = o_digamma(NN - yy + b) - o_digamma(b);
+    double S = o_digamma(phi) - o_digamma(NN + phi);
+    double Qa = o_trigamma(yy + a) - o_trigamma(a);
+    double Qb = o_trigamma(NN - yy + b) - o_trigamma(b);
+    double S1 = o_trigamma(phi) - o_trigamma(NN + phi);
+    double lD = phi * (Pa - Pb);
+    double lF = D * Pa + omD * Pb + S;
+    double lDD = phi * phi * (Qa + Qb);
+    double lDF = (Pa - Pb) + phi * (D * Qa - omD * Qb);
+    double lFF = D * D * Qa + omD * omD * Qb + S1;
+    double dD[3] = {Dq, DA, Dc};
+    for (int j = 0; j < 3; j++) {
+      G[j] += lD * dD[j];
+      for (int m = 0; m < 3; m++) Hh[j][m] += lDD * dD[j] * dD[m];
+      Hh[j][3] += lDF * dD[j];
+    }
+    Hh[P_Q][P_Q] += lD * Dqq;
+    Hh[P_Q][P_A] += lD * DqA;
+    Hh[P_A][P_Q] += lD * DqA;
+    G[3] += lF;
+    Hh[3][3] += lFF;
+  }
+  if (infeasible) {
+    r->F = INFINITY;
+    r->mag = 0;
+    for (int j = 0; j < 4; j++) {
+      r->g[j] = 0;
+      for (int m = 0; m < 4; m++) r->H[j][m] = 0;
+    }
+    return;
+  }
+  for (int j = 0; j < 3; j++) Hh[3][j] = Hh[j][3];
+
+  /* chain rule to u-space: theta = (q, A, c, phi), dtheta/du = J, d2theta/du2 = J2 */
+  double J[4] = {q * omq, A * omA, c * omc, delta};
+  double J2[4] = {q * omq * (omq - q), A * omA * (omA - A), c * omc * (omc - c), delta};
+  /* log prior (constants dropped): ln q + 2 ln(1-q) [+ ln A + 2 ln(1-A) + 8 ln(1-c)] - delta/1000 */
+  double lq = -softplus(-u[P_Q]);
+  double lp = lq + 2.0 * l1mq - delta / 1000.0;
+  double gp[4] = {1.0 - 3.0 * q, 0, 0, -delta / 1000.0};
+  double hp[4] = {-3.0 * q * omq, 0, 0, -delta / 1000.0};
+  if (model == M_PMD) {
+    lp += -softplus(-u[P_A]) + 2.0 * (-softplus(u[P_A])) + 8.0 * (-softplus(u[P_C]));
+    gp[P_A] = 1.0 - 3.0 * A;
+    hp[P_A] = -3.0 * A * omA;
+    gp[P_C] = -8.0 * c;
+    hp[P_C] = -8.0 * c * omc;
+  }
+  r->F = -(L + lp);
+  r->mag = mag;
+  for (int j = 0; j < 4; j++) {
+    r->g[j] = -(J[j] * G[j] + gp[j]);
+    for (int m = 0; m < 4; m++) {
+      double h = J[j] * Hh[j][m] * J[m];
+      if (j == m) h += J2[j] * G[j] + hp[j];
+      r->H[j][m] = -h;
+    }
+  }
+  if (model == M_NULL) { /* A, c are not parameters of model_null */
+    for (int j = 1; j <= 2; j++) {
+      r->g[j] = 0;
+      for (int m = 0; m < 4; m++) r->H[j][m] = r->H[m][j] = 0;
+    }
+  }
+}
+
+/* pooled ratio (sum y + 0.5) / (sum N + 1) over points i in [lo,hi) with
+ * kmin <= |z|-1 <= kmax */
+static double pooled(const uint32_t* y, const uint32_t* N, int lo, int hi,
+                     int kmin, int kmax) {
+  double sy = 0, sn = 0;
+  for (int i = lo; i < hi; i++) {
+    int k = kpos(i);
+    if (k >= kmin && k <= kmax) {
+      sy += y[i];
+      sn += N[i];
+    }
+  }
+  return (sy + 0.5) / (sn + 1.0);
+}
+
+static double clampd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+static double logit(double p) { return log(p) - log1p(-p); }
+
+static void init_u(int model, const uint32_t* y, const uint32_t* N, int lo,
+                   int hi, double u[4]) {
+  u[P_A] = 0;
+  u[P_C] = 0;
+  u[P_D] = log(100.0);
+  if (model == M_NULL) {
+    u[P_Q] = logit(clampd(pooled(y, N, lo, hi, 0, 99), 1e-4, 0.9));
+    return;
+  }
+  double c0 = clampd(pooled(y, N, lo, hi, 9, 99), 1e-4, 0.3);
+  double r1 = pooled(y, N, lo, hi, 0, 0);
+  double r2 = pooled(y, N, lo, hi, 1, 1);
+  double A0 = clampd(r1 - c0, 1e-3, 0.9 * (1.0 - c0));
+  double q0 = 1.0 / 3.0;
+  if (r1 - c0 > 1e-3) q0 = clampd(1.0 - (r2 - c0) / (r1 - c0), 0.05, 0.95);
+  u[P_Q] = logit(q0);
+  u[P_A] = logit(A0);
+  u[P_C] = logit(c0);
+}
+
+/* projected, Hessian-modified Newton direction */
+static void direction(int model, const double u[4], const double g[4],
+                      double H[4][4], double d[4]) {
+  int fr[4];
+  for (int j = 0; j < 4; j++) {
+    int fixed = (model == M_NULL && (j == P_A || j == P_C));
+    int act = (u[j] <= U_LO[j] && g[j] > 0) || (u[j] >= U_HI[j] && g[j] < 0);
+    fr[j] = !(fixed || act);
+  }
+  double sc = 0;
+  for (int j = 0; j < 4; j++)
+    if (fr[j] && fabs(H[j][j]) > sc) sc = fabs(H[j][j]);
+  if (sc == 0) sc = 1.0;
+  double mu = 0.0;
+  double Lc[4][4];
+  int ok = 0;
+  for (int attempt = 0; attempt < 40; attempt++) {
+    ok = 1;
+    for (int j = 0; j < 4 && ok; j++) {
+      for (int m = 0; m <= j; m++) {
+        double s;
+        if (!fr[j] || !fr[m]) s = (j == m) ? 1.0 : 0.0;
+        else s = H[j][m] + ((j == m) ? mu : 0.0);
+        for (int p = 0; p < m; p++) s -= Lc[j][p] * Lc[m][p];
+        if (j == m) {
+          if (!(s > 0)) { ok = 0; break; }
+          Lc[j][j] = sqrt(s);
+        } else {
+          Lc[j][m] = s / Lc[m][m];
+        }
+      }
+    }
+    if (ok) break;
+    mu = (mu == 0.0) ? 1e-10 * sc : mu * 10.0;
+  }
+  double rhs[4], z[4];
+  for (int j = 0; j < 4; j++) rhs[j] = fr[j] ? -g[j] : 0.0;
+  if (!ok) { /* no usable curvature (non-finite Hessian): steepest descent */
+    for (int j = 0; j < 4; j++) d[j] = isfinite(rhs[j]) ? rhs[j] : 0.0;
+    goto cap;
+  }
+  for (int j = 0; j < 4; j++) {
+    double s = rhs[j];
+    for (int p = 0; p < j; p++) s -= Lc[j][p] * z[p];
+    z[j] = s / Lc[j][j];
+  }
+  for (int j = 3; j >= 0; j--) {
+    double s = z[j];
+    for (int p = j + 1; p < 4; p++) s -= Lc[p][j] * d[p];
+    d[j] = s / Lc[j][j];
+  }
+cap:;
+  double mx = 0;
+  for (int j = 0; j < 4; j++)
+    if (fabs(d[j]) > mx) mx = fabs(d[j]);
+  if (mx > 4.0)
+    for (int j = 0; j < 4; j++) d[j] *= 4.0 / mx;
+}
+
+static double maxabs4(const double v[4]) {
+  double m = 0;
+  for (int j = 0; j < 4; j++)
+    if (fabs(v[j]) > m) m = fabs(v[j]);
+  return m;
+}
+
+typedef struct {
+  double u[4];
+  evalres r;
+  int evals;
+  int status;
+} fitres;
+
+static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
+                    int hi, int max_iter, double tol, fitres* out) {
+  double u[4], d[4], ut[4], t = 1.0;
+  evalres cur, tr;
+  init_u(model, y, N, lo, hi, u);
+  evaluate(model, y, N, lo, hi, u, &cur);
+  int evals = 1, status = MDFIT_MAXITER;
+  if (!isfinite(cur.F)) {
+    status = MDFIT_NONFINITE;
+    goto done;
+  }
+  direction(model, u, cur.g, cur.H, d);
+  if (maxabs4(d) <= tol) {
+    status = MDFIT_OK;
+    goto done;
+  }
+  while (evals < max_iter) {
+    for (int j = 0; j < 4; j++) ut[j] = clampd(u[j] + t * d[j], U_LO[j], U_HI[j]);
+    evaluate(model, y, N, lo, hi, ut, &tr);
+    evals++;
+    int acc = isfinite(tr.F) &&
+              (tr.F < cur.F ||
+               (tr.F <= cur.F + 4e-15 * cur.mag && maxabs4(tr.g) < maxabs4(cur.g)));
+    if (acc) {
+      memcpy(u, ut, sizeof(u));
+      cur = tr;
+      direction(model, u, cur.g, cur.H, d);
+      t = 1.0;
+      if (maxabs4(d) <= tol) {
+        status = MDFIT_OK;
+        break;
+      }
+    } else {
+      t *= 0.5;
+      if (t < 1e-12) { /* line search exhausted: numerically at the optimum */
+        status = (maxabs4(d) <= 1e-5) ? MDFIT_OK : MDFIT_MAXITER;
+        break;
+      }
+    }
+  }
+done:
+  memcpy(out->u, u, sizeof(u));
+  out->r = cur;
+  out->evals = evals;
+  out->status = status;
+}
+
+/* n_sigma of fits.py:194-201 with one posterior "sample" (the mode):
+ * lppd_i = ell_i, pWAIC_i = 0, waic_i = -2 ell_i (fits.py:147-172) */
+static double n_sigma(const double* lP, const double* lN, int n) {
+  double d[NPOS], md = 0, wP = 0, wN = 0;
+  for (int i = 0; i < n; i++) {
+    d[i] = (-2.0 * lP[i]) - (-2.0 * lN[i]);
+    md += d[i];
+    wP += -2.0 * lP[i];
+    wN += -2.0 * lN[i];
+  }
+  md /= n;
+  double v = 0;
+  for (int i = 0; i < n; i++) v += (d[i] - md) * (d[i] - md);
+  v /= n;
+  return (wN - wP) / sqrt(n * v);
+}
+
+/* compute_assymmetry_combined_vs_forwardreverse, fits.py:204-227 */
+static double asymmetry(const double* lC, const double* lF, const double* lR) {
+  double d[NPOS], md = 0, wC = 0, wFR = 0;
+  for (int i = 0; i < NPOS; i++) {
+    double fr = (i < NHALF) ? lF[i] : lR[i];
+    d[i] = (-2.0 * lC[i]) - (-2.0 * fr);
+    md += d[i];
+    wC += -2.0 * lC[i];
+    wFR += -2.0 * fr;
+  }
+  md /= NPOS;
+  double v = 0;
+  for (int i = 0; i < NPOS; i++) v += (d[i] - md) * (d[i] - md);
+  v /= NPOS;
+  return (wFR - wC) / sqrt(NPOS * v);
+}
+
+/* add_noise_estimates, fits.py:359-376: columns AC AG AT CA CG CT GA GC GT TA TC TG */
+static void noise(const uint32_t* mm, double out3[3]) {
+  double X[NPOS][12];
+  int valid[NPOS][12];
+  for (int j = 0; j < 12; j++) {
+    double s = 0;
+    int cnt = 0;
+    for (int i = 0; i < NPOS; i++) {
+      int nanned = (j == 5 && i < NHALF) || (j == 6 && i >= NHALF);
+      valid[i][j] = !nanned;
+      if (!nanned) {
+        s += mm[i * 12 + j];
+        cnt++;
+      }
+    }
+    double m = s / cnt;
+    for (int i = 0; i < NPOS; i++) {
+      X[i][j] = mm[i * 12 + j] / m;
+      if (valid[i][j] && isnan(X[i][j])) valid[i][j] = 0;
+    }
+  }
+  int ranges[3][2] = {{0, NPOS}, {0, NHALF}, {NHALF, NPOS}};
+  for (int r = 0; r < 3; r++) {
+    double s = 0;
+    int cnt = 0;
+    for (int i = ranges[r][0]; i < ranges[r][1]; i++)
+      for (int j = 0; j < 12; j++)
+        if (valid[i][j]) {
+          s += X[i][j];
+          cnt++;
+        }
+    if (cnt == 0) {
+      out3[r] = NAN;
+      continue;
+    }
+    double mean = s / cnt, v = 0;
+    for (int i = ranges[r][0]; i < ranges[r][1]; i++)
+      for (int j = 0; j < 12; j++)
+        if (valid[i][j]) v += (X[i][j] - mean) * (X[i][j] - mean);
+    out3[r] = sqrt(v / cnt);
+  }
+}
+
+#define Z68 0.994457883209753 /* Phi^-1(0.84): 68 % central interval */
+
+/* MAP predictive summary at point i: median := D(z), HPDI := D -/+ Z68 * sd of
+ * BetaBinomial(D phi, (1-D) phi, N)/N, clipped to [0,1]; NaN when N = 0
+ * (the reference divides 0 draws by N = 0, fits.py:115). */
+static void predict(double A, double q, double c, double phi, int k, double N,
+                    double o[3]) {
+  if (N == 0) {
+    o[0] = o[1] = o[2] = NAN;
+    return;
+  }
+  double D = A * pow(1.0 - q, k) + c;
+  if (D > 1.0) D = 1.0;
+  double sd = sqrt(D * (1.0 - D) * (phi + N) / (N * (phi + 1.0)));
+  o[0] = D;
+  o[1] = clampd(D - Z68 * sd, 0.0, 1.0);
+  o[2] = clampd(D + Z68 * sd, 0.0, 1.0);
+}
+
+static void fit_taxon(const uint32_t* y, const uint32_t* N, const uint32_t* mm,
+                      const mdfit_opts* o, double* out, float* pred, int32_t* status) {
+  for (int j = 0; j < MDFIT_NOUT; j++) out[j] = 0.0;
+  for (int i = 0; i < NPOS; i++)
+    if (y[i] > N[i]) {
+      for (int j = 0; j < MDFIT_NOUT; j++) out[j] = NAN;
+      if (pred)
+        for (int j = 0; j < 3 * NPOS; j++) pred[j] = NAN;
+      *status = MDFIT_INVALID;
+      return;
+    }
+  static const int models[6] = {M_PMD, M_NULL, M_PMD, M_PMD, M_NULL, M_NULL};
+  static const int los[6] = {0, 0, 0, NHALF, 0, NHALF};
+  static const int his[6] = {NPOS, NPOS, NHALF, NPOS, NHALF, NPOS};
+  fitres f[6];
+  int st = MDFIT_OK;
+  for (int s = 0; s < 6; s++) {
+    fit_one(models[s], y, N, los[s], his[s], o->max_iter, o->tol_step, &f[s]);
+    if (f[s].status > st) st = f[s].status;
+    double* dg = out + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * s;
+    dg[0] = sigm(f[s].u[P_Q]);
+    dg[1] = models[s] == M_PMD ? sigm(f[s].u[P_A]) : 0.0;
+    dg[2] = models[s] == M_PMD ? sigm(f[s].u[P_C]) : 0.0;
+    dg[3] = exp(f[s].u[P_D]) + 2.0;
+    dg[4] = f[s].r.F;
+    dg[5] = f[s].evals;
+    dg[6] = f[s].status;
+    dg[7] = 0.0;
+  }
+  double p[3];
+  /* PMD-all: predictions + D_max (fits.py:249-261: median / HPDI at z = +1) */
+  double qa = out[MDFIT_F_DIAG + 0], Aa = out[MDFIT_F_DIAG + 1];
+  double ca = out[MDFIT_F_DIAG + 2], pa = out[MDFIT_F_DIAG + 3];
+  for (int i = 0; i < NPOS; i++) {
+    predict(Aa, qa, ca, pa, kpos(i), (double)N[i], p);
+    if (pred)
+      for (int r = 0; r < 3; r++) pred[r * NPOS + i] = (float)p[r];
+    if (i == 0) {
+      out[MDFIT_F_D_MAX] = p[0];
+      out[MDFIT_F_D_MAX_LOWER_HPDI] = p[1];
+      out[MDFIT_F_D_MAX_UPPER_HPDI] = p[2];
+    }
+  }
+  out[MDFIT_F_N_SIGMA] = n_sigma(f[0].r.ell, f[1].r.ell, NPOS);
+  out[MDFIT_F_Q_MEAN] = qa;
+  out[MDFIT_F_CONCENTRATION_MEAN] = pa;
+  out[MDFIT_F_D_MAX_MARGINALIZED_MEAN] = Aa + ca;
+  double nf = 0, nr = 0, yf = 0, yr = 0;
+  for (int i = 0; i < NHALF; i++) {
+    nf += N[i];
+    yf += y[i];
+    nr += N[NHALF + i];
+    yr += y[NHALF + i];
+  }
+  out[MDFIT_F_N_Z1_FORWARD] = N[0];
+  out[MDFIT_F_N_Z1_REVERSE] = N[NHALF];
+  out[MDFIT_F_N_SUM_FORWARD] = nf;
+  out[MDFIT_F_N_SUM_REVERSE] = nr;
+  out[MDFIT_F_N_SUM_TOTAL] = nf + nr;
+  out[MDFIT_F_Y_SUM_FORWARD] = yf;
+  out[MDFIT_F_Y_SUM_REVERSE] = yr;
+  out[MDFIT_F_Y_SUM_TOTAL] = yf + yr;
+  /* forward (fits.py:311-329) */
+  out[MDFIT_F_N_SIGMA_FORWARD] = n_sigma(f[2].r.ell, f[4].r.ell, NHALF);
+  {
+    const double* dg = out + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * 2;
+    predict(dg[1], dg[0], dg[2], dg[3], 0, (double)N[0], p);
+    out[MDFIT_F_D_MAX_FORWARD] = p[0];
+    out[MDFIT_F_Q_MEAN_FORWARD] = dg[0];
+  }
+  /* reverse (fits.py:333-350); D_max_reverse evaluated on data_forward (:343-348) */
+  out[MDFIT_F_N_SIGMA_REVERSE] =
+      n_sigma(f[3].r.ell + NHALF, f[5].r.ell + NHALF, NHALF);
+  {
+    const double* dg = out + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * 3;
+    predict(dg[1], dg[0], dg[2], dg[3], 0, (double)N[0], p);
+    out[MDFIT_F_D_MAX_REVERSE] = p[0];
+    out[MDFIT_F_Q_MEAN_REVERSE] = dg[0];
+  }
+  out[MDFIT_F_ASYMMETRY] = asymmetry(f[0].r.ell, f[2].r.ell, f[3].r.ell);
+  if (mm) {
+    double nz[3];
+    noise(mm, nz);
+    out[MDFIT_F_NORMALIZED_NOISE] = nz[0];
+    out[MDFIT_F_NORMALIZED_NOISE_FORWARD] = nz[1];
+    out[MDFIT_F_NORMALIZED_NOISE_REVERSE] = nz[2];
+  } else {
+    out[MDFIT_F_NORMALIZED_NOISE] = out[MDFIT_F_NORMALIZED_NOISE_FORWARD] =
+        out[MDFIT_F_NORMALIZED_NOISE_REVERSE] = NAN;
+  }
+  *status = st;
+}
+
+/* Host-pointer batch fit: same layout as mdfit_fit_batch.  OpenMP over taxa;
+ * n_threads <= 0 -> OpenMP default. */
+int oracle_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm,
+                     int64_t n_taxa, const mdfit_opts* opts, double* out,
+                     float* pred, int32_t* status, int n_threads) {
+  mdfit_opts o;
+  memset(&o, 0, sizeof(o));
+  o.max_iter = 200;
+  o.tol_step = 1e-9;
+  if (opts) o = *opts;
+#ifdef _OPENMP
+  int nt = n_threads > 0 ? n_threads : omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 4) num_threads(nt)
+#endif
+  for (int64_t t = 0; t < n_taxa; t++) {
+    fit_taxon(y + t * MDFIT_LD, N + t * MDFIT_LD,
+              mm ? mm + t * NPOS * MDFIT_NMM : NULL, &o, out + t * MDFIT_NOUT,
+              pred ? pred + t * MDFIT_NPRED * NPOS : NULL, status + t);
+  }
+  return 0;
+}
+
+/* Objective / gradient / Hessian at u for one sub-fit (scipy cross-checks).
+ * model 0 = PMD, 1 = null; subset 0 = all, 1 = fwd, 2 = rev. */
+void oracle_objective(int model, int subset, const uint32_t* y, const uint32_t* N,
+                      const double* u, double* F, double* g4, double* H16,
+                      double* ell30) {
+  int lo = subset == 2 ? NHALF : 0, hi = subset == 1 ? NHALF : NPOS;
+  evalres r;
+  memset(&r, 0, sizeof(r));
+  evaluate(model, y, N, lo, hi, u, &r);
+  *F = r.F;
+  for (int j = 0; j < 4; j++) {
+    g4[j] = r.g[j];
+    for (int m = 0; m < 4; m++) H16[4 * j + m] = r.H[j][m];
+  }
+  if (ell30)
+    for (int i = 0; i < NPOS; i++) ell30[i] = (i >= lo && i < hi) ? r.ell[i] : 0.0;
+}
+
+/* One sub-fit from the spec's initial point; returns u*, F*, evals, status. */
+void oracle_fit_subfit(int model, int subset, const uint32_t* y, const uint32_t* N,
+                       int max_iter, double tol, double* u4, double* F,
+                       int32_t* evals, int32_t* status) {
+  int lo = subset == 2 ? NHALF : 0, hi = subset == 1 ? NHALF : NPOS;
+  fitres f;
+  fit_one(model, y, N, lo, hi, max_iter, tol, &f);
+  for (int j = 0; j < 4; j++) u4[j] = f.u[j];
+  *F = f.r.F;
+  *evals = f.evals;
+  *status = f.status;
+}
+
+/* Initial point of the spec (for tests). */
+void oracle_init_u(int model, int subset, const uint32_t* y, const uint32_t* N, double* u4) {
+  int lo = subset == 2 ? NHALF : 0, hi = subset == 1 ? NHALF : NPOS;
+  init_u(model, y, N, lo, hi, u4);
+}

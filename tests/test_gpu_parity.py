@@ -1,0 +1,190 @@
+"""GPU parity tests: the HIP path (through the C-ABI) vs the CPU oracle and the
+committed golden vectors.  Run on an MI355X: pytest -m gpu."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from tests.helpers import RTOL, mixed_rel, mm_from_counts_parquet, pack_golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test selected but no HIP device is visible")
+    from metadamage_amd import engine as eng
+
+    return eng
+
+
+def _result_parity(out, ref_out, fields=slice(0, 25)):
+    rel = mixed_rel(out[:, fields], ref_out[:, fields])
+    return float(rel.max()) if rel.size else 0.0
+
+
+# --------------------------------------------------------------------------
+# special functions and the beta-binomial log-pmf vs scipy known answers
+# --------------------------------------------------------------------------
+def test_special_functions_vs_scipy(engine, scipy_golden):
+    x = scipy_golden["special_x"]
+    o = engine.special(x)
+    for j, key in enumerate(("special_lgamma", "special_digamma", "special_trigamma")):
+        ref = scipy_golden[key]
+        err = np.abs(o[:, j] - ref) / np.maximum(1.0, np.abs(ref))
+        assert err.max() < 1e-13, (key, err.max(), x[err.argmax()])
+
+
+def test_betabinom_logpmf_vs_scipy(engine, scipy_golden):
+    g = scipy_golden
+    lp, grad = engine.betabinom_logpmf(g["bb_y"], g["bb_N"], g["bb_a"], g["bb_b"])
+    ref = g["bb_logpmf"]
+    # lgamma of arguments up to 1e9 carries ~2e-16 * 2e10 absolute rounding
+    err = np.abs(lp - ref) / np.maximum(1.0, np.abs(ref))
+    assert err.max() < 1e-10, err.max()
+    for j, key in enumerate(("bb_dalpha", "bb_dbeta")):
+        e = np.abs(grad[:, j] - g[key]) / np.maximum(1e-6, np.abs(g[key]))
+        assert e.max() < 1e-8, (key, e.max())
+
+
+# --------------------------------------------------------------------------
+# the fit vs the oracle
+# --------------------------------------------------------------------------
+def test_fixture_taxa_vs_oracle(engine, oracle_lib, ref_golden):
+    names = ["data_ancient", "data_control"]
+    y, N = pack_golden(ref_golden, names)
+    mm = np.concatenate([mm_from_counts_parquet(n) for n in names])
+    out, pred, st = engine.fit_batch(y, N, mm)
+    ref_out, ref_pred, ref_st = oracle_lib.fit_batch(y, N, mm)
+    assert (st == 0).all() and (ref_st == 0).all()
+    assert _result_parity(out, ref_out) < 1e-8
+    assert np.nanmax(mixed_rel(pred, ref_pred)) < 1e-6
+
+
+def test_synthetic_vs_oracle(engine, oracle_lib):
+    from metadamage_amd.synthetic import generate
+
+    b = generate(2000, seed=1)
+    out, pred, st = engine.fit_batch(b.y, b.N, b.mm)
+    ref_out, ref_pred, ref_st = oracle_lib.fit_batch(b.y, b.N, b.mm)
+    assert (st == ref_st).all()
+    rel = mixed_rel(out[:, :25], ref_out[:, :25])
+    assert rel.max() < RTOL, (rel.max(), np.unravel_index(rel.argmax(), rel.shape))
+    # p99.9 is far tighter than the bar: same algorithm, FP64 on both sides
+    assert np.quantile(rel, 0.999) < 1e-8
+    # fitted parameters of all 6 sub-fits (q, A, c on their scale; phi on log scale)
+    for s in range(6):
+        base = 32 + 8 * s
+        for j in range(3):
+            assert mixed_rel(out[:, base + j], ref_out[:, base + j]).max() < RTOL
+        dlphi = np.abs(np.log(out[:, base + 3]) - np.log(ref_out[:, base + 3]))
+        assert dlphi.max() < RTOL
+    assert np.nanmax(mixed_rel(pred, ref_pred)) < 1e-5
+
+
+def test_record_vs_reference_assembly(engine, ref_golden, ref_meta):
+    """The record assembled by the reference's own compute_fit_results
+    (fits.py:230-356) with MAP quantities injected at the numpyro boundary."""
+    keys = ref_meta["record_keys"][3:]
+    from metadamage_amd._lib import RESULT_FIELDS
+
+    for name in ("data_ancient", "data_control", "synthetic"):
+        y, N = pack_golden(ref_golden, [name])
+        mm = mm_from_counts_parquet(name)
+        out, pred, st = engine.fit_batch(y, N, mm)
+        rec = ref_golden[f"record_{name}__values"]
+        n = rec.shape[0]
+        for k in keys:
+            if k == "N_alignments":
+                continue
+            j = RESULT_FIELDS.index(k)
+            rel = mixed_rel(out[:n, j], rec[:, keys.index(k)])
+            assert rel.max() < RTOL, (name, k, rel.max())
+        med = ref_golden[f"record_{name}__median"]
+        hp = ref_golden[f"record_{name}__hpdi"]
+        assert np.nanmax(mixed_rel(pred[:n, 0], med)) < 1e-5
+        assert np.nanmax(mixed_rel(pred[:n, 1], hp[:, 0])) < 1e-5
+        assert np.nanmax(mixed_rel(pred[:n, 2], hp[:, 1])) < 1e-5
+        noise = ref_golden[f"{name}__noise"]
+        assert np.nanmax(mixed_rel(out[:n, 22:25], noise)) < 1e-10
+
+
+# --------------------------------------------------------------------------
+# edge cases (empty / ragged / extreme inputs)
+# --------------------------------------------------------------------------
+def _edge_batch():
+    from metadamage_amd.synthetic import generate
+
+    b = generate(16, seed=9)
+    y, N, mm = b.y.copy(), b.N.copy(), b.mm.copy()
+    N[0, :30] = 0  # no coverage at all
+    y[0, :30] = 0
+    N[1, 5:12] = 0  # ragged coverage
+    y[1, 5:12] = 0
+    N[2, 0] = 0  # N_z1 = 0 -> D_max NaN like the reference's 0/0
+    y[2, 0] = 0
+    y[3, :30] = N[3, :30]  # y == N everywhere
+    y[4, :30] = 0  # no damage signal at all
+    N[5, :30] = 4_000_000_000  # near the uint32 ceiling
+    y[5, :30] = (N[5, :30] // 100).astype(np.uint32)
+    y[6, 3] = N[6, 3] + 1  # invalid -> status 3
+    N[7, :30] = 1  # minimal coverage
+    y[7, :30] = np.arange(30) % 2
+    mm[8] = 0  # all mismatch columns zero -> noise NaN
+    return y, N, mm
+
+
+def test_edge_cases_vs_oracle(engine, oracle_lib):
+    y, N, mm = _edge_batch()
+    out, pred, st = engine.fit_batch(y, N, mm)
+    ref_out, ref_pred, ref_st = oracle_lib.fit_batch(y, N, mm)
+    assert (st == ref_st).all(), (st, ref_st)
+    assert st[6] == 3 and np.isnan(out[6, :25]).all()
+    ok = st != 3
+    rel = mixed_rel(out[ok, :25], ref_out[ok, :25])
+    assert rel.max() < RTOL, (rel.max(), np.unravel_index(rel.argmax(), rel.shape))
+    assert np.isnan(out[2, 0]) and np.isnan(ref_out[2, 0])
+    assert np.isnan(out[8, 22:25]).all()
+
+
+def test_empty_batch(engine):
+    from metadamage_amd import _lib
+
+    lib = _lib.load()
+    assert lib.mdfit_fit_batch(None, None, None, 0, None, None, None, None, None, None) == 0
+
+
+def test_no_mismatch_counts_gives_nan_noise(engine):
+    from metadamage_amd.synthetic import generate
+
+    b = generate(8, seed=4)
+    out, _, st = engine.fit_batch(b.y, b.N, None)
+    assert (st == 0).all()
+    assert np.isnan(out[:, 22:25]).all()
+
+
+# --------------------------------------------------------------------------
+# size-independent properties at the benchmark size (10k taxa, config C2)
+# --------------------------------------------------------------------------
+def test_bench_size_properties(engine, oracle_lib):
+    from metadamage_amd.synthetic import generate
+
+    b = generate(10_000, seed=1)
+    out1, pred1, st1 = engine.fit_batch(b.y, b.N, b.mm)
+    out2, pred2, st2 = engine.fit_batch(b.y, b.N, b.mm)
+    # deterministic: bit-identical reruns
+    assert np.array_equal(out1, out2, equal_nan=True) and np.array_equal(st1, st2)
+    # order-independent: a permuted batch gives the same per-taxon bits
+    perm = np.random.default_rng(0).permutation(b.n_taxa)
+    out3, _, st3 = engine.fit_batch(b.y[perm], b.N[perm], b.mm[perm])
+    assert np.array_equal(out3, out1[perm], equal_nan=True)
+    assert (st1 == 0).mean() > 0.999
+    # a seeded 400-taxon sample against the oracle
+    idx = np.sort(np.random.default_rng(1).choice(b.n_taxa, 400, replace=False))
+    ref_out, _, ref_st = oracle_lib.fit_batch(b.y[idx], b.N[idx], b.mm[idx])
+    assert (ref_st == st1[idx]).all()
+    assert mixed_rel(out1[idx, :25], ref_out[:, :25]).max() < RTOL
