@@ -156,6 +156,18 @@ int mdfit_betabinom_logpmf(const double* y, const double* N, const double* alpha
 int mdfit_special(const double* x, int64_t n, double* out3, void* hip_stream);
 
 /*
+ * Objective of one sub-fit at given unconstrained parameters, evaluated by
+ * the fit kernel's own lane layout and code (parity tests).  Per item i:
+ * model[i] (0 PMD, 1 null), subset[i] (0 all, 1 forward, 2 reverse),
+ * y/N rows [n][MDFIT_LD], u[n][4] = (logit q, logit A, logit c, log delta).
+ * Outputs F[n] = -(sum ell + log prior), g[n][4], H[n][4][4] (d/du),
+ * ell[n][30] (pointwise log-lik without log C(N,y); 0 outside the subset).
+ */
+int mdfit_objective(const int32_t* model, const int32_t* subset, const uint32_t* y,
+                    const uint32_t* N, const double* u, int64_t n, double* F, double* g,
+                    double* H, double* ell, void* hip_stream);
+
+/*
  * Register-only throughput probe of the per-point evaluation the fit kernel
  * runs (value + gradient + Hessian of one beta-binomial point): launches
  * `n_waves` waves that each do `iters` evaluations; `sink` is a device

@@ -68,6 +68,7 @@ EXPORTED_SYMBOLS = [
     "mdfit_betabinom_logpmf",
     "mdfit_special",
     "mdfit_peak_probe",
+    "mdfit_objective",
     "mdfit_last_error",
     "mdfit_abi_version",
 ]
@@ -116,6 +117,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.mdfit_special.restype = ctypes.c_int
     lib.mdfit_peak_probe.argtypes = [i64, i32, vp, vp]
     lib.mdfit_peak_probe.restype = ctypes.c_int
+    lib.mdfit_objective.argtypes = [vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp]
+    lib.mdfit_objective.restype = ctypes.c_int
     lib.mdfit_last_error.argtypes = []
     lib.mdfit_last_error.restype = ctypes.c_char_p
     lib.mdfit_abi_version.argtypes = []

@@ -39,14 +39,24 @@ constexpr int kLD = MDFIT_LD;
 constexpr int kNMM = MDFIT_NMM;
 constexpr double kZ68 = 0.994457883209753;  // Phi^-1(0.84)
 
-__constant__ double kULo[4] = {-25.0, -25.0, -25.0, -25.0};
-__constant__ double kUHi[4] = {25.0, 25.0, 25.0, 20.0};
+// u = (logit q, logit A, c, log delta): c on its own scale (see oracle).
+__constant__ double kULo[4] = {-25.0, -25.0, 0.0, -25.0};
+__constant__ double kUHi[4] = {25.0, 25.0, 0.999, 20.0};
+constexpr double kEpsAct = 1e-8;
+constexpr double kNoiseF = 1.4e-14;  // objective rounding scale (oracle: NOISE_F)
 
 // ---------------------------------------------------------------------------
 // cross-lane sums inside aligned groups of G lanes (G = 16 or 32)
 // ---------------------------------------------------------------------------
+// The leading empty asm makes `v` opaque: without it hipcc (fp-contract=fast)
+// fuses the producer's multiply into the first butterfly add on THIS lane only
+// (fma(a, b, partner) vs partner's rounded a*b), so lanes of one group end up
+// with sums that differ in the last bit and their Newton state machines drift
+// apart.  With both operands already rounded every step is a commutative add
+// and all G lanes hold bitwise-identical sums.
 template <int G>
 __device__ __forceinline__ double gsum(double v) {
+  asm volatile("" : "+v"(v));
 #pragma unroll
   for (int m = G / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
   return v;
@@ -83,7 +93,7 @@ __device__ __forceinline__ void point_eval(const PointData& pd, const double u[4
   double D, Dq, DA, Dc, Dqq, DqA;
   if (pd.pmd) {
     const double A = sigm(u[1]);
-    const double c = sigm(u[2]);
+    const double c = u[2];
     const double kk = (double)pd.k;
     const double wq = exp((kk - 1.0) * l1mq);  // (1-q)^(k-1)
     const double w = exp(kk * l1mq);
@@ -147,7 +157,7 @@ __device__ __forceinline__ void finish_eval(bool pmd, const double u[4], const d
                                             Eval& e) {
   const double q = sigm(u[0]), omq = sigm(-u[0]);
   const double A = pmd ? sigm(u[1]) : 0.0, omA = pmd ? sigm(-u[1]) : 1.0;
-  const double c = pmd ? sigm(u[2]) : 0.0, omc = pmd ? sigm(-u[2]) : 1.0;
+  const double c = pmd ? u[2] : 0.0, omc = 1.0 - c;
   const double delta = exp(u[3]);
   const double G[4] = {s[2], s[3], s[4], s[5]};
   double Hh[4][4];
@@ -161,17 +171,17 @@ __device__ __forceinline__ void finish_eval(bool pmd, const double u[4], const d
   Hh[2][2] = s[13];
   Hh[2][3] = Hh[3][2] = s[14];
   Hh[3][3] = s[15];
-  const double J[4] = {q * omq, A * omA, c * omc, delta};
-  const double J2[4] = {q * omq * (omq - q), A * omA * (omA - A), c * omc * (omc - c), delta};
+  const double J[4] = {q * omq, A * omA, 1.0, delta};
+  const double J2[4] = {q * omq * (omq - q), A * omA * (omA - A), 0.0, delta};
   double lp = -softplus(-u[0]) - 2.0 * softplus(u[0]) - delta / 1000.0;
   double gp[4] = {1.0 - 3.0 * q, 0.0, 0.0, -delta / 1000.0};
   double hp[4] = {-3.0 * q * omq, 0.0, 0.0, -delta / 1000.0};
   if (pmd) {
-    lp += -softplus(-u[1]) - 2.0 * softplus(u[1]) - 8.0 * softplus(u[2]);
+    lp += -softplus(-u[1]) - 2.0 * softplus(u[1]) + 8.0 * log1p(-c);
     gp[1] = 1.0 - 3.0 * A;
     hp[1] = -3.0 * A * omA;
-    gp[2] = -8.0 * c;
-    hp[2] = -8.0 * c * omc;
+    gp[2] = -8.0 / omc;
+    hp[2] = -8.0 / (omc * omc);
   }
   const bool infeasible = pmd && (A + c >= 1.0);
   e.F = infeasible ? INFINITY : -(s[0] + lp);
@@ -200,15 +210,38 @@ __device__ __forceinline__ double maxabs4(const double v[4]) {
   return fmax(fmax(fabs(v[0]), fabs(v[1])), fmax(fabs(v[2]), fabs(v[3])));
 }
 
-// Projected, Hessian-modified Newton direction (oracle: direction()).
+// projected-gradient size (oracle: pgnorm): 0 for a variable held on its bound
+__device__ __forceinline__ double pgnorm(const double u[4], const double g[4]) {
+  double m = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) m = fmax(m, fabs(u[j] - clampd(u[j] - g[j], kULo[j], kUHi[j])));
+  return m;
+}
+
+__constant__ double kEpsBind[4] = {1e-3, 1e-3, 1e-4, 1e-3};
+
+// Projected, Hessian-modified Newton direction with a Bertsekas binding set
+// (oracle: direction()): variables within eps of a bound and pushed outward
+// step onto the bound and leave the Newton system.
 __device__ void newton_dir(bool pmd, const double u[4], const double g[4], const double H[4][4],
                            double d[4]) {
   bool fr[4];
+  double dbind[4];
+  double w = 0.0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const bool fixed = !pmd && (j == 1 || j == 2);
-    const bool act = (u[j] <= kULo[j] && g[j] > 0.0) || (u[j] >= kUHi[j] && g[j] < 0.0);
-    fr[j] = !(fixed || act);
+    if (!fixed) w = fmax(w, fabs(u[j] - clampd(u[j] - g[j], kULo[j], kUHi[j])));
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool fixed = !pmd && (j == 1 || j == 2);
+    const double eps = fmin(kEpsBind[j], w);
+    const bool atlo = u[j] - kULo[j] <= eps, athi = kUHi[j] - u[j] <= eps;
+    // on / next to a box bound and not pulled inward by more than kEpsAct
+    const bool bind = (atlo && g[j] > -kEpsAct) || (athi && g[j] < kEpsAct);
+    dbind[j] = (bind && !fixed) ? (atlo ? kULo[j] : kUHi[j]) - u[j] : 0.0;
+    fr[j] = !(fixed || bind);
   }
   double sc = 0.0;
 #pragma unroll
@@ -266,12 +299,22 @@ __device__ void newton_dir(bool pmd, const double u[4], const double g[4], const
       d[j] = s / Lc[j][j];
     }
   }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (!fr[j]) d[j] = dbind[j];
   const double mx = maxabs4(d);
   if (mx > 4.0) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) d[j] *= 4.0 / mx;
   }
 }
+
+#ifdef MDFIT_TRACE
+// debug-only build (-DMDFIT_TRACE): per-iteration trace of one taxon's fits
+__device__ double* g_trace = nullptr;
+__device__ int64_t g_trace_taxon = -1;
+__device__ int g_trace_phase = 0;
+#endif
 
 // Result of one group's fit, replicated on every lane of the group.
 struct FitOut {
@@ -317,7 +360,8 @@ __device__ FitOut run_fits(const PointData& pd, const double u0[4], int max_iter
       } else {
         accept = isfinite(tr.F) &&
                  (tr.F < cur.F ||
-                  (tr.F <= cur.F + 4e-15 * cur.mag && maxabs4(tr.g) < maxabs4(cur.g)));
+                  (tr.F <= cur.F + kNoiseF * (cur.mag + fabs(cur.F)) &&
+                   pgnorm(ut, tr.g) < pgnorm(u, cur.g)));
       }
       if (accept) {
 #pragma unroll
@@ -347,6 +391,23 @@ __device__ FitOut run_fits(const PointData& pd, const double u0[4], int max_iter
 #pragma unroll
         for (int j = 0; j < 4; ++j) ut[j] = clampd(u[j] + t * d[j], kULo[j], kUHi[j]);
       }
+#ifdef MDFIT_TRACE
+      if (g_trace != nullptr && (int64_t)blockIdx.x == g_trace_taxon && evals <= 200) {
+        const int grp = G == 32 ? (threadIdx.x >> 5) : 2 + (threadIdx.x >> 4);
+        double* r = g_trace + ((int64_t)grp * 200 + (evals - 1)) * 64;
+        r[32 + (threadIdx.x % G)] = ell;
+        r[16 + (threadIdx.x % G) % 16] = ut[0];
+      }
+      if (g_trace != nullptr && (int64_t)blockIdx.x == g_trace_taxon && (threadIdx.x % G) == 0 &&
+          evals <= 200) {
+        const int grp = G == 32 ? (threadIdx.x >> 5) : 2 + (threadIdx.x >> 4);
+        double* r = g_trace + ((int64_t)grp * 200 + (evals - 1)) * 64;
+        r[0] = tr.F; r[1] = cur.F; r[2] = accept; r[3] = t; r[4] = maxabs4(d);
+        r[5] = maxabs4(tr.g); r[6] = maxabs4(cur.g); r[7] = cur.mag; r[8] = done; r[9] = status;
+        for (int j = 0; j < 4; ++j) { r[10 + j] = u[j]; }
+        r[14] = d[0]; r[15] = d[3];
+      }
+#endif
     }
   }
 #pragma unroll
@@ -384,7 +445,7 @@ __device__ void init_point(const PointData& pd, double u0[4]) {
   if (r1 - c0 > 1e-3) q0 = clampd(1.0 - (r2 - c0) / (r1 - c0), 0.05, 0.95);
   u0[0] = logit(q0);
   u0[1] = logit(A0);
-  u0[2] = logit(c0);
+  u0[2] = c0;
 }
 
 // MAP predictive summary of one point (oracle: predict()).
@@ -414,6 +475,32 @@ __device__ __forceinline__ double nsigma_group(bool valid, double lP, double lN,
   const double dd = v * (d - md);
   const double var = gsum<G>(dd * dd) / n;
   return (wN - wP) / sqrt(n * var);
+}
+
+// Lane -> point maps of the two phases (see the header comment).
+__device__ __forceinline__ PointData phase_a_point(int lane, const double* s_y, const double* s_N) {
+  PointData pd;
+  const int p = lane & 31;
+  pd.valid = p < kNPos;
+  const int pi = pd.valid ? p : 0;
+  pd.y = s_y[pi];
+  pd.N = s_N[pi];
+  pd.k = pi < kNHalf ? pi : pi - kNHalf;
+  pd.pmd = lane < 32;
+  return pd;
+}
+
+__device__ __forceinline__ PointData phase_b_point(int lane, const double* s_y, const double* s_N) {
+  PointData pd;
+  const int row = lane >> 4, p = lane & 15;
+  const bool rev = row & 1;
+  pd.valid = p < kNHalf;
+  const int pi = (pd.valid ? p : 0) + (rev ? kNHalf : 0);
+  pd.y = s_y[pi];
+  pd.N = s_N[pi];
+  pd.k = pd.valid ? p : 0;
+  pd.pmd = lane < 32;
+  return pd;
 }
 
 constexpr int kBlock = 64;  // one wave = one taxon
@@ -456,21 +543,14 @@ __global__ __launch_bounds__(kBlock) void fit_map_kernel(
   // ======================= phase A: PMD-all | null-all =======================
   double ellPall;  // lane p < 30: PMD-all pointwise log-lik at the mode
   {
-    PointData pd;
-    const int p = lane & 31;
-    pd.valid = p < kNPos;
-    const int pi = pd.valid ? p : 0;
-    pd.y = s_y[pi];
-    pd.N = s_N[pi];
-    pd.k = pi < kNHalf ? pi : pi - kNHalf;
-    pd.pmd = lane < 32;
+    const PointData pd = phase_a_point(lane, s_y, s_N);
     double u0[4];
     init_point<32>(pd, u0);
     const FitOut f = run_fits<32>(pd, u0, max_iter, tol);
     ellPall = f.ell;
     const double q = sigm(f.u[0]);
     const double A = pd.pmd ? sigm(f.u[1]) : 0.0;
-    const double c = pd.pmd ? sigm(f.u[2]) : 0.0;
+    const double c = pd.pmd ? f.u[2] : 0.0;
     const double phi = exp(f.u[3]) + 2.0;
     // diagnostics: sub-fit 0 (PMD-all) from lane 0, sub-fit 1 (null-all) from lane 32
     if (lane == 0 || lane == 32) {
@@ -508,21 +588,14 @@ __global__ __launch_bounds__(kBlock) void fit_map_kernel(
 
   // ================ phase B: PMD-fwd | PMD-rev | null-fwd | null-rev =========
   {
-    PointData pd;
     const int row = lane >> 4, p = lane & 15;
-    const bool rev = row & 1;
-    pd.valid = p < kNHalf;
-    const int pi = (pd.valid ? p : 0) + (rev ? kNHalf : 0);
-    pd.y = s_y[pi];
-    pd.N = s_N[pi];
-    pd.k = pd.valid ? p : 0;
-    pd.pmd = lane < 32;
+    const PointData pd = phase_b_point(lane, s_y, s_N);
     double u0[4];
     init_point<16>(pd, u0);
     const FitOut f = run_fits<16>(pd, u0, max_iter, tol);
     const double q = sigm(f.u[0]);
     const double A = pd.pmd ? sigm(f.u[1]) : 0.0;
-    const double c = pd.pmd ? sigm(f.u[2]) : 0.0;
+    const double c = pd.pmd ? f.u[2] : 0.0;
     const double phi = exp(f.u[3]) + 2.0;
     if (p == 0) {  // lanes 0, 16, 32, 48 -> sub-fits 2, 3, 4, 5
       double* dg = s_rec + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * (2 + row);
@@ -702,6 +775,64 @@ __global__ __launch_bounds__(kBlock) void peak_probe_kernel(int iters, double* _
   sink[(int64_t)blockIdx.x * kBlock + lane] = accum;
 }
 
+// Objective / gradient / Hessian of one sub-fit at a given u, evaluated with
+// exactly the lane layout and code of the fit kernel (parity tests of the
+// objective itself).  One wave per item.
+__global__ __launch_bounds__(kBlock) void objective_kernel(
+    const int32_t* __restrict__ model, const int32_t* __restrict__ subset,
+    const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN, const double* __restrict__ gu,
+    int64_t n, double* __restrict__ F, double* __restrict__ g, double* __restrict__ H,
+    double* __restrict__ ell_out) {
+  __shared__ double s_y[kLD], s_N[kLD];
+  const int lane = threadIdx.x;
+  const int64_t i = blockIdx.x;
+  if (i >= n) return;
+  if (lane < kLD) {
+    s_y[lane] = (double)gy[i * kLD + lane];
+    s_N[lane] = (double)gN[i * kLD + lane];
+  }
+  __syncthreads();
+  const int m = model[i], sub = subset[i];
+  double u[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) u[j] = gu[i * 4 + j];
+  double acc[kNAcc], ell;
+  Eval e;
+  int lead, point;
+  bool mine;
+  if (sub == 0) {
+    const PointData pd = phase_a_point(lane, s_y, s_N);
+    point_eval(pd, u, acc, ell);
+#pragma unroll
+    for (int k = 0; k < kNAcc; ++k) acc[k] = gsum<32>(acc[k]);
+    finish_eval(pd.pmd, u, acc, e);
+    lead = m == 0 ? 0 : 32;
+    mine = (lane >> 5) == (lead >> 5) && pd.valid;
+    point = lane & 31;
+  } else {
+    const PointData pd = phase_b_point(lane, s_y, s_N);
+    point_eval(pd, u, acc, ell);
+#pragma unroll
+    for (int k = 0; k < kNAcc; ++k) acc[k] = gsum<16>(acc[k]);
+    finish_eval(pd.pmd, u, acc, e);
+    lead = 16 * ((m == 0 ? 0 : 2) + (sub == 2 ? 1 : 0));
+    mine = (lane >> 4) == (lead >> 4) && pd.valid;
+    point = (lane & 15) + (sub == 2 ? kNHalf : 0);
+  }
+  if (lane < kNPos) ell_out[i * kNPos + lane] = 0.0;
+  __syncthreads();
+  if (mine) ell_out[i * kNPos + point] = ell;
+  if (lane == lead) {
+    F[i] = e.F;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      g[i * 4 + j] = e.g[j];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) H[i * 16 + 4 * j + k] = e.H[j][k];
+    }
+  }
+}
+
 }  // namespace mdfit
 
 // ===========================================================================
@@ -787,6 +918,25 @@ int mdfit_peak_probe(int64_t n_waves, int32_t iters, double* sink, void* hip_str
                      (hipStream_t)hip_stream, iters, sink);
   return check_launch("peak_probe_kernel");
 }
+
+int mdfit_objective(const int32_t* model, const int32_t* subset, const uint32_t* y,
+                    const uint32_t* N, const double* u, int64_t n, double* F, double* g,
+                    double* H, double* ell, void* hip_stream) {
+  if (n < 0 || (n > 0 && (!model || !subset || !y || !N || !u || !F || !g || !H || !ell)))
+    return set_err(MDFIT_E_ARG, "bad arguments");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(mdfit::objective_kernel, dim3((unsigned)n), dim3(mdfit::kBlock), 0,
+                     (hipStream_t)hip_stream, model, subset, y, N, u, n, F, g, H, ell);
+  return check_launch("objective_kernel");
+}
+
+#ifdef MDFIT_TRACE
+int mdfit_set_trace(double* buf, int64_t taxon) {
+  hipMemcpyToSymbol(HIP_SYMBOL(mdfit::g_trace), &buf, sizeof(buf));
+  hipMemcpyToSymbol(HIP_SYMBOL(mdfit::g_trace_taxon), &taxon, sizeof(taxon));
+  return 0;
+}
+#endif
 
 const char* mdfit_last_error(void) { return g_err; }
 

@@ -141,3 +141,25 @@ def peak_probe(n_waves: int, iters: int, stream=None):
     sink = torch.empty(n_waves * 64, dtype=torch.float64, device="cuda")
     _lib.check(lib.mdfit_peak_probe(n_waves, iters, ctypes.c_void_p(sink.data_ptr()), _stream_handle(torch, stream)))
     return sink
+
+
+def objective(model, subset, y, N, u, device="cuda"):
+    """Per-item sub-fit objective (F, g[4], H[4,4], ell[30]) evaluated by the
+    fit kernel's code path (mdfit_objective)."""
+    torch = _torch()
+    lib = _lib.load()
+    n = len(model)
+    tm = torch.as_tensor(np.ascontiguousarray(model, dtype=np.int32), device=device)
+    ts = torch.as_tensor(np.ascontiguousarray(subset, dtype=np.int32), device=device)
+    ty = torch.from_numpy(np.ascontiguousarray(y, dtype=np.uint32).view(np.int32)).to(device)
+    tN = torch.from_numpy(np.ascontiguousarray(N, dtype=np.uint32).view(np.int32)).to(device)
+    tu = torch.as_tensor(np.ascontiguousarray(u, dtype=np.float64), device=device)
+    F = torch.empty(n, dtype=torch.float64, device=device)
+    g = torch.empty((n, 4), dtype=torch.float64, device=device)
+    H = torch.empty((n, 4, 4), dtype=torch.float64, device=device)
+    ell = torch.empty((n, 30), dtype=torch.float64, device=device)
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    _lib.check(lib.mdfit_objective(ptr(tm), ptr(ts), ptr(ty), ptr(tN), ptr(tu), n, ptr(F), ptr(g), ptr(H),
+                                   ptr(ell), _stream_handle(torch)))
+    torch.cuda.current_stream().synchronize()
+    return F.cpu().numpy(), g.cpu().numpy(), H.cpu().numpy(), ell.cpu().numpy()

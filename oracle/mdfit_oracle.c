@@ -117,8 +117,16 @@ void oracle_betabinom_logpmf(const double* y, const double* N, const double* a,
 enum { M_PMD = 0, M_NULL = 1 };
 enum { P_Q = 0, P_A = 1, P_C = 2, P_D = 3 }; /* u-space parameter slots */
 
-static const double U_LO[4] = {-25.0, -25.0, -25.0, -25.0};
-static const double U_HI[4] = {25.0, 25.0, 25.0, 20.0};
+/* u = (logit q, logit A, c, log delta); c is optimised on its own scale so a
+ * background rate that the data do not support lands exactly on c = 0 (the
+ * mode of its Beta(1,9) prior) in one projected step instead of an
+ * exponentially slow walk down logit c. */
+static const double U_LO[4] = {-25.0, -25.0, 0.0, -25.0};
+static const double U_HI[4] = {25.0, 25.0, 0.999, 20.0};
+#define EPS_ACT 1e-8
+/* rounding scale of the objective: a trial whose F is within NOISE_F*(sum |lnGamma| + |F|)
+ * of the current one is accepted when it lowers the projected gradient */
+#define NOISE_F 1.4e-14
 
 static double softplus(double x) { return (x > 0 ? x : 0.0) + log1p(exp(-fabs(x))); }
 static double sigm(double u) { return 1.0 / (1.0 + exp(-u)); }
@@ -144,8 +152,8 @@ static void evaluate(int model, const uint32_t* y, const uint32_t* N, int lo,
   if (model == M_PMD) {
     A = sigm(u[P_A]);
     omA = sigm(-u[P_A]);
-    c = sigm(u[P_C]);
-    omc = sigm(-u[P_C]);
+    c = u[P_C];
+    omc = 1.0 - c;
   }
   double delta = exp(u[P_D]);
   double phi = delta + 2.0;
@@ -218,19 +226,19 @@ static void evaluate(int model, const uint32_t* y, const uint32_t* N, int lo,
   for (int j = 0; j < 3; j++) Hh[3][j] = Hh[j][3];
 
   /* chain rule to u-space: theta = (q, A, c, phi), dtheta/du = J, d2theta/du2 = J2 */
-  double J[4] = {q * omq, A * omA, c * omc, delta};
-  double J2[4] = {q * omq * (omq - q), A * omA * (omA - A), c * omc * (omc - c), delta};
+  double J[4] = {q * omq, A * omA, 1.0, delta};
+  double J2[4] = {q * omq * (omq - q), A * omA * (omA - A), 0.0, delta};
   /* log prior (constants dropped): ln q + 2 ln(1-q) [+ ln A + 2 ln(1-A) + 8 ln(1-c)] - delta/1000 */
   double lq = -softplus(-u[P_Q]);
   double lp = lq + 2.0 * l1mq - delta / 1000.0;
   double gp[4] = {1.0 - 3.0 * q, 0, 0, -delta / 1000.0};
   double hp[4] = {-3.0 * q * omq, 0, 0, -delta / 1000.0};
   if (model == M_PMD) {
-    lp += -softplus(-u[P_A]) + 2.0 * (-softplus(u[P_A])) + 8.0 * (-softplus(u[P_C]));
+    lp += -softplus(-u[P_A]) + 2.0 * (-softplus(u[P_A])) + 8.0 * log1p(-c);
     gp[P_A] = 1.0 - 3.0 * A;
     hp[P_A] = -3.0 * A * omA;
-    gp[P_C] = -8.0 * c;
-    hp[P_C] = -8.0 * c * omc;
+    gp[P_C] = -8.0 / omc;
+    hp[P_C] = -8.0 / (omc * omc);
   }
   r->F = -(L + lp);
   r->mag = mag;
@@ -285,17 +293,34 @@ static void init_u(int model, const uint32_t* y, const uint32_t* N, int lo,
   if (r1 - c0 > 1e-3) q0 = clampd(1.0 - (r2 - c0) / (r1 - c0), 0.05, 0.95);
   u[P_Q] = logit(q0);
   u[P_A] = logit(A0);
-  u[P_C] = logit(c0);
+  u[P_C] = c0;
 }
 
-/* projected, Hessian-modified Newton direction */
+/* projected, Hessian-modified Newton direction (Bertsekas-style binding set):
+ * a variable within eps of a bound whose gradient pushes it outward is moved
+ * onto the bound (d = bound - u) and removed from the Newton system; the
+ * others take the (Hessian-modified) Newton step of the reduced system. */
+static const double EPS_BIND[4] = {1e-3, 1e-3, 1e-4, 1e-3};
+
 static void direction(int model, const double u[4], const double g[4],
                       double H[4][4], double d[4]) {
   int fr[4];
+  double dbind[4] = {0, 0, 0, 0};
+  double w = 0; /* projected-gradient size */
+  for (int j = 0; j < 4; j++) {
+    if (model == M_NULL && (j == P_A || j == P_C)) continue;
+    double pg = fabs(u[j] - clampd(u[j] - g[j], U_LO[j], U_HI[j]));
+    if (pg > w) w = pg;
+  }
   for (int j = 0; j < 4; j++) {
     int fixed = (model == M_NULL && (j == P_A || j == P_C));
-    int act = (u[j] <= U_LO[j] && g[j] > 0) || (u[j] >= U_HI[j] && g[j] < 0);
-    fr[j] = !(fixed || act);
+    double eps = EPS_BIND[j] < w ? EPS_BIND[j] : w;
+    int atlo = u[j] - U_LO[j] <= eps, athi = U_HI[j] - u[j] <= eps;
+    /* a variable on (or next to) its box bound stays there unless the
+     * objective pulls it inward by more than EPS_ACT */
+    int bind = (atlo && g[j] > -EPS_ACT) || (athi && g[j] < EPS_ACT);
+    if (bind && !fixed) dbind[j] = (atlo ? U_LO[j] : U_HI[j]) - u[j];
+    fr[j] = !(fixed || bind);
   }
   double sc = 0;
   for (int j = 0; j < 4; j++)
@@ -340,11 +365,24 @@ static void direction(int model, const double u[4], const double g[4],
     d[j] = s / Lc[j][j];
   }
 cap:;
+  for (int j = 0; j < 4; j++)
+    if (!fr[j]) d[j] = dbind[j];
   double mx = 0;
   for (int j = 0; j < 4; j++)
     if (fabs(d[j]) > mx) mx = fabs(d[j]);
   if (mx > 4.0)
     for (int j = 0; j < 4; j++) d[j] *= 4.0 / mx;
+}
+
+/* projected-gradient size max_j |u_j - clamp(u_j - g_j)|: the stationarity
+ * measure of a box-constrained problem (0 for a variable held on its bound) */
+static double pgnorm(const double u[4], const double g[4]) {
+  double m = 0;
+  for (int j = 0; j < 4; j++) {
+    double v = fabs(u[j] - clampd(u[j] - g[j], U_LO[j], U_HI[j]));
+    if (v > m) m = v;
+  }
+  return m;
 }
 
 static double maxabs4(const double v[4]) {
@@ -360,6 +398,10 @@ typedef struct {
   int evals;
   int status;
 } fitres;
+
+#include <stdio.h>
+static int g_trace = 0; /* debugging aid: print every evaluation of fit_one */
+void oracle_set_trace(int on) { g_trace = on; }
 
 static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
                     int hi, int max_iter, double tol, fitres* out) {
@@ -383,7 +425,11 @@ static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
     evals++;
     int acc = isfinite(tr.F) &&
               (tr.F < cur.F ||
-               (tr.F <= cur.F + 4e-15 * cur.mag && maxabs4(tr.g) < maxabs4(cur.g)));
+               (tr.F <= cur.F + NOISE_F * (cur.mag + fabs(cur.F)) &&
+                pgnorm(ut, tr.g) < pgnorm(u, cur.g)));
+    if (g_trace)
+      printf("%d trF=%.12f curF=%.12f acc=%d t=%.3g |d|=%.3e |gt|=%.3e |gc|=%.3e u=[%.10f %.10f %.10f %.10f] d=[%.3e %.3e %.3e %.3e]\n",
+             evals, tr.F, cur.F, acc, t, maxabs4(d), maxabs4(tr.g), maxabs4(cur.g), u[0], u[1], u[2], u[3], d[0], d[1], d[2], d[3]);
     if (acc) {
       memcpy(u, ut, sizeof(u));
       cur = tr;
@@ -526,7 +572,7 @@ static void fit_taxon(const uint32_t* y, const uint32_t* N, const uint32_t* mm,
     double* dg = out + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * s;
     dg[0] = sigm(f[s].u[P_Q]);
     dg[1] = models[s] == M_PMD ? sigm(f[s].u[P_A]) : 0.0;
-    dg[2] = models[s] == M_PMD ? sigm(f[s].u[P_C]) : 0.0;
+    dg[2] = models[s] == M_PMD ? f[s].u[P_C] : 0.0;
     dg[3] = exp(f[s].u[P_D]) + 2.0;
     dg[4] = f[s].r.F;
     dg[5] = f[s].evals;

@@ -246,7 +246,7 @@ def main():
         q = special.expit(u[0])
         phi = np.exp(u[3]) + 2.0
         if model_name == "model_PMD":
-            return (q, special.expit(u[1]), special.expit(u[2]), phi)
+            return (q, special.expit(u[1]), u[2], phi)
         return (q, 0.0, 0.0, phi)
 
     def solver(model_name, data):

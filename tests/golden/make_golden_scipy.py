@@ -31,15 +31,16 @@ sys.path.insert(0, str(ROOT))
 
 from metadamage_amd.synthetic import NHALF, NPOS, abs_z, generate  # noqa: E402
 
-U_LO = np.array([-25.0, -25.0, -25.0, -25.0])
-U_HI = np.array([25.0, 25.0, 25.0, 20.0])
+# u = (logit q, logit A, c, log delta): the box of MDFIT-MAP v1
+U_LO = np.array([-25.0, -25.0, 0.0, -25.0])
+U_HI = np.array([25.0, 25.0, 0.999, 20.0])
 
 
 def objective(u, model, y, N, lo, hi):
     """F(u) = -(sum_i ell_i + log prior) of MDFIT-MAP v1, with gradient.
 
     model_PMD / model_null of fits.py:43-67 with theta = (q, A, c, delta):
-    q, A, c = sigmoid(u), delta = exp(u_delta), phi = delta + 2; the log
+    q, A = sigmoid(u), c = u_c, delta = exp(u_delta), phi = delta + 2; the log
     prior is Beta(2,3)(q) [Beta(2,3)(A), Beta(1,9)(c)], Exponential(1/1000)(delta)
     without the Jacobian (a mode of the constrained density).
     """
@@ -51,7 +52,7 @@ def objective(u, model, y, N, lo, hi):
     phi = delta + 2.0
     if model == 0:
         A = special.expit(u[1])
-        c = special.expit(u[2])
+        c = u[2]
         if A + c >= 1.0:
             return np.inf, np.zeros(4)
         w = (1.0 - q) ** k
@@ -74,11 +75,11 @@ def objective(u, model, y, N, lo, hi):
     g_theta = np.array([np.sum(lD * dD[0]), np.sum(lD * dD[1]), np.sum(lD * dD[2]), np.sum(lF)])
     lp = np.log(q) + 2 * np.log1p(-q) - delta / 1000.0
     gp = np.array([1 - 3 * q, 0.0, 0.0, -delta / 1000.0])
-    J = np.array([q * (1 - q), A * (1 - A), c * (1 - c), delta])
+    J = np.array([q * (1 - q), A * (1 - A), 1.0, delta])
     if model == 0:
         lp += np.log(A) + 2 * np.log1p(-A) + 8 * np.log1p(-c)
         gp[1] = 1 - 3 * A
-        gp[2] = -8 * c
+        gp[2] = -8 / (1 - c)
     F = -(ell.sum() + lp)
     g = -(J * g_theta + gp)
     if model == 1:
@@ -103,7 +104,7 @@ def spec_init(model, y, N, lo, hi):
     r1, r2 = r(k == 0), r(k == 1)
     A0 = np.clip(r1 - c0, 1e-3, 0.9 * (1 - c0))
     q0 = np.clip(1 - (r2 - c0) / (r1 - c0), 0.05, 0.95) if r1 - c0 > 1e-3 else 1.0 / 3.0
-    return np.array([special.logit(q0), special.logit(A0), special.logit(c0), np.log(100.0)])
+    return np.array([special.logit(q0), special.logit(A0), c0, np.log(100.0)])
 
 
 def _newton_polish(fun, x, lo, hi, iters=60):
@@ -119,7 +120,7 @@ def _newton_polish(fun, x, lo, hi, iters=60):
             e[j] = h
             H[:, j] = (fun(np.clip(x + e, lo, hi))[1] - fun(np.clip(x - e, lo, hi))[1]) / (2 * h)
         H = 0.5 * (H + H.T)
-        act = ((x <= lo) & (g > 0)) | ((x >= hi) & (g < 0))
+        act = ((x <= lo) & (g > -1e-8)) | ((x >= hi) & (g < 1e-8))
         fr = ~act
         d = np.zeros(n)
         if fr.any():
@@ -179,10 +180,10 @@ def map_fit(model, y, N, lo, hi, starts):
 def starts_for(model):
     """Fixed extra starts (besides the spec's initial point)."""
     rng = np.random.default_rng(7)
-    base = [[-0.7, -2.0, -4.0, np.log(100.0)], [0.0, -4.0, -6.0, np.log(1000.0)],
-            [1.0, -1.0, -3.0, np.log(20.0)], [-4.0, -3.0, -5.0, np.log(5000.0)]]
+    base = [[-0.7, -2.0, 0.02, np.log(100.0)], [0.0, -4.0, 0.002, np.log(1000.0)],
+            [1.0, -1.0, 0.05, np.log(20.0)], [-4.0, -3.0, 0.0, np.log(5000.0)]]
     for _ in range(2):
-        base.append([rng.uniform(-6, 2), rng.uniform(-5, -0.5), rng.uniform(-8, -2), rng.uniform(1, 9)])
+        base.append([rng.uniform(-6, 2), rng.uniform(-5, -0.5), rng.uniform(0.0, 0.1), rng.uniform(1, 9)])
     if model == 1:
         base = [[b[0], 0.0, 0.0, b[3]] for b in base]
     return base
