@@ -1,0 +1,233 @@
+"""Benchmark: TaxID damage fits/s of the MI355X MAP fit engine (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1]): 10,000 synthetic TaxIDs
+per GPU x 30 positions (z = +-1..15), seed 1 (+ rank), MAP beta-binomial fit of
+model_PMD and model_null on all / forward / reverse positions (the 6 sub-fits
+the reference runs per TaxID, fits.py:438-439, 311-313, 333-335), the record
+assembly, noise estimates and per-position predictions.  One step = one
+mdfit_fit_batch launch over the rank's shard with inputs already resident in HBM,
+plus (N > 1) the single RCCL gather of the packed result records to rank 0.
+Weak scaling: every rank fits its own 10,000 taxa.
+
+Printed JSON (rank 0): the driver contract fields plus
+  roofline          HBM roofline of the fit kernel (algorithmic bytes / kernel
+                    time, HIP events on the launch stream; traffic from the
+                    committed rocprofv3 PMC pass, profiles/)
+  compute_roofline  useful point-evaluations/s vs the register-only probe of the
+                    same point evaluation (the kernel's real bound: FP64 VALU)
+  cpu_baseline      the CPU oracle (C/OpenMP restatement of the same fit,
+                    oracle/mdfit_oracle.c) on the same 10k-taxon workload
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+TAXA_PER_GPU = 10_000
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# algorithmic bytes per taxon: y,N 2x30x4 + mismatch 30x12x4 in,
+# 25 result fields x8 + predictions 3x30x4 + status 4 out
+ALG_BYTES_PER_TAXON = 240 + 1440 + 200 + 360 + 4
+NPTS = np.array([30, 30, 15, 15, 15, 15])
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--taxa", type=int, default=TAXA_PER_GPU, help="taxa per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    return ap.parse_args()
+
+
+def pmc_traffic():
+    """Per-launch HBM bytes of the fit kernel from the committed rocprofv3 PMC
+    summary (profiles/pmc_fit_map_kernel.json), or None."""
+    f = ROOT / "profiles" / "pmc_fit_map_kernel.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from metadamage_amd import _lib, engine
+    from metadamage_amd.distributed import REC_BYTES, alloc_records, gather_records, packed_views
+    from metadamage_amd.synthetic import generate
+
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    # ---- synthetic shard, resident in HBM before timing -------------------
+    T = args.taxa
+    b = generate(T, seed=1 + rank)
+    ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm, device=dev)
+    rec = alloc_records(T, dev)
+    out, pred, status = packed_views(rec, T)
+    res = engine.FitBatch(out, pred, status)
+    opts = _lib.default_opts()
+    stream = torch.cuda.current_stream(dev)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        engine.fit_batch_device(ty, tN, tm, opts, res, stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:
+            gather_records(rec, T, rank, world)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(events[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kernel_ms = np.array([a.elapsed_time(b_) for a, b_ in events])
+
+    # per-rank diagnostics of the last step
+    o = out.cpu().numpy()
+    st = status.cpu().numpy()
+    evals = o[:, _lib.F_DIAG + 5 :: _lib.DIAG_STRIDE][:, :6]
+    useful_pe = float((evals * NPTS).sum())
+    lane_pe = float(64 * (np.maximum(evals[:, 0], evals[:, 1]) + evals[:, 2:].max(1)).sum())
+
+    if rank == 0:
+        total = T * world * args.steps
+        value = total / elapsed
+        k_avg_s = float(kernel_ms.mean()) / 1e3
+        achieved = ALG_BYTES_PER_TAXON * T / k_avg_s / 1e9
+        traffic = pmc_traffic()
+        # compute roofline: register-only probe of the same point evaluation
+        n_waves, iters = 256 * 16, 64
+        engine.peak_probe(n_waves, iters, stream=stream)  # warm
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(3):
+            engine.peak_probe(n_waves, iters, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        probe_rate = 3 * n_waves * 64 * iters / (e0.elapsed_time(e1) / 1e3)
+        useful_rate = useful_pe / k_avg_s
+        line = {
+            "metric": "TaxID damage fits/sec",
+            "value": round(value, 1),
+            "unit": "fits/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SURVEY.md §8(d) generator, seed 1+rank)",
+            "config": {
+                "workload": "C2: 10k synthetic TaxIDs x +-15 positions per GPU, MAP beta-binomial damage fit "
+                "(model_PMD + model_null on all/forward/reverse = 6 sub-fits per TaxID) + record assembly",
+                "taxa_per_gpu": T,
+                "positions": 30,
+                "parallelism": f"taxon-shard x{world}" + (" + RCCL gather" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 3),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "fit_map_kernel",
+                "kernel_ms_avg": round(float(kernel_ms.mean()), 4),
+                "bytes_per_taxon": ALG_BYTES_PER_TAXON,
+            },
+            "compute_roofline": {
+                "bound": "fp64-valu",
+                "achieved": round(useful_rate, 1),
+                "peak": round(probe_rate, 1),
+                "unit": "point-evals/s",
+                "frac": useful_rate / probe_rate,
+                "lane_slot_frac": (lane_pe / k_avg_s) / probe_rate,
+                "point_evals_per_taxon": useful_pe / T,
+            },
+            "status_ok_frac": float((st == 0).mean()),
+        }
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(b, args.cpu_threads)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(b, threads: int):
+    """The CPU oracle (oracle/libmdfit_oracle.c, C + OpenMP, same algorithm)
+    on the same workload, timed on this host's cores."""
+    from oracle.oracle import OracleLib
+
+    lib = OracleLib()
+    nthr = threads if threads > 0 else min(16, os.cpu_count() or 1)
+    lib.fit_batch(b.y[:200], b.N[:200], b.mm[:200], threads=nthr)  # warm
+    t0 = time.perf_counter()
+    lib.fit_batch(b.y, b.N, b.mm, threads=nthr)
+    dt = time.perf_counter() - t0
+    n1 = 500
+    t1 = time.perf_counter()
+    lib.fit_batch(b.y[:n1], b.N[:n1], b.mm[:n1], threads=1)
+    d1 = time.perf_counter() - t1
+    return {
+        "value": round(b.n_taxa / dt, 1),
+        "unit": "fits/s",
+        "cores": nthr,
+        "kind": "port",
+        "sample": f"all {b.n_taxa} taxa of the rank-0 workload on {nthr} OpenMP threads ({dt:.2f} s); "
+        f"1-thread rate on the first {n1}: {n1 / d1:.1f} fits/s",
+        "single_thread_value": round(n1 / d1, 1),
+    }
+
+
+if __name__ == "__main__":
+    main()
