@@ -1,0 +1,225 @@
+"""The drop-in fit boundary: get_fits / compute_fits over the HIP engine.
+
+Mirrors /root/reference/metadamage/fits.py at its operator boundary:
+
+  get_fits(df_counts, cfg)        fits.py:754-807  (cache check, top-N, fit, save)
+  get_top_max_fits                fits.py:736-751
+  compute_fits(df_counts, cfg)    fits.py:709-730  -> ONE batched device call
+  make_df_fit_results_*           fits.py:668-680
+  make_df_fit_predictions_*       fits.py:632-665
+
+What changes is the body of compute_fits: instead of a process pool running
+numpyro NUTS per taxon (fits.py:477-626), the counts table is packed once into
+the dense layout of include/mdfit.h (the batched group_to_numpyro_data,
+fits.py:398-419) and fitted by mdfit_fit_batch on the GPU(s); taxa the engine
+flags (status != 0) are dropped with a warning, like the reference drops taxa
+whose fit timed out (fits.py:520-522, 603-606).
+"""
+
+from __future__ import annotations
+
+import logging
+
+import numpy as np
+import pandas as pd
+
+from . import _lib, io, utils
+
+logger = logging.getLogger(__name__)
+
+MM_COLUMNS = ["AC", "AG", "AT", "CA", "CG", "CT", "GA", "GC", "GT", "TA", "TC", "TG"]
+POSITIONS = np.concatenate([np.arange(1, 16), -np.arange(1, 16)])
+
+# fit_results column order (fits.py:244-293, 317-356, 374-376 + :671)
+FIT_RESULT_COLUMNS = (
+    ["tax_id", "tax_name", "tax_rank"]
+    + _lib.RESULT_FIELDS[:7]
+    + ["N_alignments"]
+    + _lib.RESULT_FIELDS[7:]
+    + ["shortname"]
+)
+INT_RESULT_FIELDS = {"N_alignments", "N_z1_forward", "N_z1_reverse", "N_sum_forward", "N_sum_reverse",
+                     "N_sum_total", "y_sum_forward", "y_sum_reverse", "y_sum_total"}
+
+
+# --------------------------------------------------------------------------
+# packing: df_counts -> dense [T][32] tensors (batched group_to_numpyro_data)
+# --------------------------------------------------------------------------
+class Packed:
+    def __init__(self, tax_id, tax_name, tax_rank, N_alignments, y, N, mm):
+        self.tax_id = tax_id
+        self.tax_name = tax_name
+        self.tax_rank = tax_rank
+        self.N_alignments = N_alignments
+        self.y = y
+        self.N = N
+        self.mm = mm
+
+    @property
+    def n_taxa(self):
+        return len(self.tax_id)
+
+
+def pack_counts(df: pd.DataFrame, cfg) -> Packed:
+    """Dense y/N (uint32[T][32]) and mismatch counts (uint32[T][30][12]) in
+    df order (first appearance of each tax_id, i.e. the N_alignments-desc
+    order of sort_by_alignments).  Column i < 15 holds z = i+1 (y = the
+    forward substitution, N = its reference-base sum), i >= 15 holds
+    z = -(i-14) (reverse substitution) — group_to_numpyro_data, fits.py:398-419.
+    Rows are placed by their position value, so missing positions read as
+    N = 0 (no information) instead of shifting the others."""
+    fwd, rev = cfg.substitution_bases_forward, cfg.substitution_bases_reverse
+    tax = df["tax_id"].to_numpy()
+    uniq, first_idx, inv = np.unique(tax, return_index=True, return_inverse=True)
+    order = np.argsort(first_idx, kind="stable")  # taxa in first-appearance order
+    rank = np.empty_like(order)
+    rank[order] = np.arange(order.size)
+    t = rank[inv]
+    T = uniq.size
+    pos = df["position"].to_numpy().astype(np.int64)
+    col = np.where(pos > 0, pos - 1, 14 - pos)
+    ok = (pos != 0) & (np.abs(pos) <= 15)
+    if not ok.all():
+        logger.warning(f"{int((~ok).sum())} rows with |position| outside 1..15 ignored")
+    y = np.zeros((T, _lib.LD), np.uint64)
+    N = np.zeros((T, _lib.LD), np.uint64)
+    yv = np.where(pos > 0, df[fwd].to_numpy(), df[rev].to_numpy()).astype(np.uint64)
+    Nv = np.where(pos > 0, df[fwd[0]].to_numpy(), df[rev[0]].to_numpy()).astype(np.uint64)
+    y[t[ok], col[ok]] = yv[ok]
+    N[t[ok], col[ok]] = Nv[ok]
+    if y.max(initial=0) > np.iinfo(np.uint32).max or N.max(initial=0) > np.iinfo(np.uint32).max:
+        raise AssertionError("Dataframe contains too large values.")  # as utils.py:338-339
+    mm = np.zeros((T, _lib.NPOS, _lib.NMM), np.uint32)
+    mm[t[ok], col[ok], :] = df[MM_COLUMNS].to_numpy()[ok].astype(np.uint32)
+    first = first_idx[order]
+    return Packed(
+        tax_id=uniq[order],
+        tax_name=df["tax_name"].to_numpy()[first],
+        tax_rank=df["tax_rank"].to_numpy()[first],
+        N_alignments=df["N_alignments"].to_numpy()[first].astype(np.int64),
+        y=y.astype(np.uint32),
+        N=N.astype(np.uint32),
+        mm=mm,
+    )
+
+
+# --------------------------------------------------------------------------
+# the device call (single GPU or sharded over torch.distributed ranks)
+# --------------------------------------------------------------------------
+def fit_packed(p: Packed, opts=None):
+    """Run mdfit_fit_batch on the packed taxa; returns host (out, pred, status)
+    on rank 0 (None elsewhere in a multi-GPU job)."""
+    import torch
+
+    from . import engine
+    from .distributed import alloc_records, gather_records, packed_views, shard_capacity, shard_range
+    from .distributed import unpack_gathered
+
+    if not torch.cuda.is_available():
+        raise _lib.MdfitError("metadamage_amd fits run on MI355X GPUs only (no HIP device visible)")
+    import torch.distributed as dist
+
+    world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    rank = dist.get_rank() if world > 1 else 0
+    dev = torch.device("cuda", torch.cuda.current_device())
+    if world == 1:
+        return engine.fit_batch(p.y, p.N, p.mm, opts)
+    lo, hi = shard_range(p.n_taxa, rank, world)
+    cap = shard_capacity(p.n_taxa, world)
+    rec = alloc_records(cap, dev)
+    out, pred, status = packed_views(rec, cap)
+    if hi > lo:
+        ty, tN, tm = engine.to_device_counts(p.y[lo:hi], p.N[lo:hi], p.mm[lo:hi], device=dev)
+        engine.fit_batch_device(ty, tN, tm, opts, engine.FitBatch(out[: hi - lo], pred[: hi - lo],
+                                                                   status[: hi - lo]))
+    torch.cuda.synchronize(dev)
+    parts = gather_records(rec, cap, rank, world)
+    if rank != 0:
+        return None
+    return unpack_gathered(parts, p.n_taxa, world)
+
+
+# --------------------------------------------------------------------------
+# frames (fits.py:632-680)
+# --------------------------------------------------------------------------
+def make_df_fit_results(p: Packed, out, keep, cfg) -> pd.DataFrame:
+    data = {
+        "tax_id": p.tax_id[keep],
+        "tax_name": p.tax_name[keep],
+        "tax_rank": p.tax_rank[keep],
+    }
+    for j, name in enumerate(_lib.RESULT_FIELDS):
+        v = out[keep, j]
+        data[name] = np.rint(v).astype(np.int64) if name in INT_RESULT_FIELDS else v
+    data["N_alignments"] = p.N_alignments[keep]
+    df = pd.DataFrame(data)[FIT_RESULT_COLUMNS[:-1]]
+    df["shortname"] = cfg.shortname
+    df = utils.downcast_dataframe(df, ["tax_id", "tax_name", "tax_rank", "shortname"], fully_automatic=False)
+    return df.reset_index(drop=True)
+
+
+def make_df_fit_predictions(p: Packed, pred, keep, cfg) -> pd.DataFrame:
+    n = int(keep.sum())
+    df = pd.DataFrame(
+        {
+            "tax_id": np.repeat(p.tax_id[keep], _lib.NPOS),
+            "position": np.tile(POSITIONS, n),
+            "median": pred[keep, 0, :].reshape(-1).astype(np.float64),
+            "hdpi_lower": pred[keep, 1, :].reshape(-1).astype(np.float64),
+            "hdpi_upper": pred[keep, 2, :].reshape(-1).astype(np.float64),
+        }
+    )
+    df["shortname"] = cfg.shortname
+    return utils.downcast_dataframe(df, ["tax_id", "shortname"], fully_automatic=False)
+
+
+def compute_fits(df_counts, cfg, mcmc_kwargs=None, opts=None):
+    """fits.py:709-730: (df_fit_results, df_fit_predictions) for every taxon of
+    df_counts, in df_counts order.  `mcmc_kwargs` is accepted for signature
+    compatibility; the MAP engine ignores it."""
+    p = pack_counts(df_counts, cfg)
+    res = fit_packed(p, opts)
+    if res is None:  # non-zero rank of a multi-GPU job
+        return None, None
+    out, pred, status = res
+    keep = status == _lib.OK
+    for t in np.where(~keep)[0]:
+        logger.warning(f"Fit: tax_id {p.tax_id[t]} failed (status {int(status[t])}). Skipping.")
+    return make_df_fit_results(p, out, keep, cfg), make_df_fit_predictions(p, pred, keep, cfg)
+
+
+def extract_top_max_fits(df_counts, max_fits):
+    """fits.py:736-744: taxa with the largest summed N_alignments (ties: first
+    in groupby order, i.e. ascending tax_id)."""
+    top = df_counts.groupby("tax_id", observed=True)["N_alignments"].sum().nlargest(max_fits).index
+    return df_counts[df_counts["tax_id"].isin(top)]
+
+
+def get_top_max_fits(df_counts, N_fits):
+    if N_fits is not None and N_fits > 0:
+        return extract_top_max_fits(df_counts, N_fits)
+    return df_counts
+
+
+CACHE_KEYS = ["min_alignments", "min_y_sum", "substitution_bases_forward", "substitution_bases_reverse",
+              "N_fits", "shortname", "filename"]
+
+
+def get_fits(df_counts, cfg, opts=None):
+    """fits.py:754-807."""
+    parquet_fit_results = io.Parquet(cfg.filename_fit_results)
+    parquet_fit_predictions = io.Parquet(cfg.filename_fit_predictions)
+    if parquet_fit_results.exists(cfg.forced) and parquet_fit_predictions.exists(cfg.forced):
+        metadata_cfg = cfg.to_dict()
+        if utils.metadata_is_similar(parquet_fit_results.load_metadata(), metadata_cfg, include=CACHE_KEYS) and \
+                utils.metadata_is_similar(parquet_fit_predictions.load_metadata(), metadata_cfg, include=CACHE_KEYS):
+            logger.info("Fit: Loading fits from parquet-file.")
+            return parquet_fit_results.load(), parquet_fit_predictions.load()
+    logger.info("Fit: Generating fits and saving to file.")
+    df_counts_top_N = get_top_max_fits(df_counts, cfg.N_fits)
+    df_fit_results, df_fit_predictions = compute_fits(df_counts_top_N, cfg, opts=opts)
+    if df_fit_results is None:
+        return None, None
+    parquet_fit_results.save(df_fit_results, metadata=cfg.to_dict())
+    parquet_fit_predictions.save(df_fit_predictions, metadata=cfg.to_dict())
+    return df_fit_results, df_fit_predictions

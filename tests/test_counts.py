@@ -1,0 +1,122 @@
+"""CPU tests: count ingest + cuts + packing vs the reference's own pipeline
+(golden tables made by tests/golden/make_golden_reference.py)."""
+
+from __future__ import annotations
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from metadamage_amd import counts, fits, utils
+from tests.helpers import GOLDEN, MM_COLUMNS
+
+CASES = {
+    "data_ancient": "data_ancient.txt",
+    "data_control": "data_control.txt",
+    "synthetic": "synthetic_counts_22col.tsv",
+    "synthetic_strict": "synthetic_counts_22col.tsv",
+    "synthetic_CA_GT": "synthetic_counts_22col.tsv",
+}
+
+
+def cfg_for(meta_case, path, out_dir="/tmp/mdfit_unused"):
+    c = meta_case["cfg"]
+    cfg = utils.Config(out_dir=out_dir, max_fits=None, max_cores=1, min_alignments=c["min_alignments"],
+                       min_y_sum=c["min_y_sum"], substitution_bases_forward=c["substitution_bases_forward"],
+                       substitution_bases_reverse=c["substitution_bases_reverse"], forced=False, version="0.0.0")
+    cfg.add_filename(path)
+    cfg.shortname = c["shortname"]
+    return cfg
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_counts_pipeline_matches_reference(name, ref_meta):
+    cfg = cfg_for(ref_meta["cases"][name], GOLDEN / CASES[name])
+    df = counts.compute_counts(cfg)
+    ref = pd.read_parquet(GOLDEN / f"counts_{name}.parquet")
+    assert list(df.columns) == list(ref.columns) == ref_meta["cases"][name]["columns"]
+    assert len(df) == len(ref)
+    for col in ref.columns:
+        if isinstance(ref[col].dtype, pd.CategoricalDtype) or ref[col].dtype == object:
+            assert (df[col].astype(str).to_numpy() == ref[col].astype(str).to_numpy()).all(), col
+        else:
+            assert np.array_equal(df[col].to_numpy().astype(float), ref[col].to_numpy().astype(float)), col
+    # pandas-1.x dtypes of the reference's downcast (utils.py:329-356)
+    assert df["position"].dtype == np.int8
+    assert df["N_alignments"].dtype == np.uint32
+    assert isinstance(df["tax_id"].dtype, pd.CategoricalDtype)
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_packing_matches_group_to_numpyro_data(name, ref_meta, ref_golden):
+    cfg = cfg_for(ref_meta["cases"][name], GOLDEN / CASES[name])
+    df = pd.read_parquet(GOLDEN / f"counts_{name}.parquet")
+    p = fits.pack_counts(df, cfg)
+    assert (p.tax_id == ref_golden[f"{name}__tax_id"]).all()
+    assert (p.y[:, :30] == ref_golden[f"{name}__y"]).all()
+    assert (p.N[:, :30] == ref_golden[f"{name}__N"]).all()
+    assert (p.y[:, 30:] == 0).all() and (p.N[:, 30:] == 0).all()
+    mm = df[MM_COLUMNS].to_numpy().reshape(-1, 30, 12)
+    assert (p.mm == mm).all()
+
+
+def test_top_max_fits_matches_reference(ref_meta):
+    for name in CASES:
+        df = pd.read_parquet(GOLDEN / f"counts_{name}.parquet")
+        df["tax_id"] = df["tax_id"].astype("category")
+        for k, expect in ref_meta["cases"][name]["top_max_fits"].items():
+            got = [int(t) for t in pd.unique(fits.get_top_max_fits(df, int(k)).tax_id)]
+            assert got == expect, (name, k)
+
+
+def test_cut_semantics_are_frozen(tmp_path):
+    """N_alignments >= min_alignments AND y_sum_total >= min_y_sum (counts.py:207-209),
+    y_sum_total = sum of the forward substitution at z > 0 + reverse at z < 0."""
+    from metadamage_amd.synthetic import generate, to_counts_table
+
+    b = generate(30, seed=21, fail_fraction=0.5)
+    table = to_counts_table(b)
+    f = tmp_path / "cut.tsv"
+    table.to_csv(f, sep="\t", header=False, index=False)
+    cfg = utils.Config(out_dir=tmp_path, max_fits=None, max_cores=1, min_alignments=50, min_y_sum=25,
+                       substitution_bases_forward="CT", substitution_bases_reverse="GA", forced=False,
+                       version="0.0.0")
+    cfg.add_filename(f)
+    df = counts.compute_counts(cfg)
+    ysum = b.y[:, :15].sum(1) + b.y[:, 15:30].sum(1)
+    keep = (b.N_alignments >= 50) & (ysum >= 25)
+    assert set(int(t) for t in pd.unique(df.tax_id)) == set(int(t) for t in b.tax_id[keep])
+    g = df.groupby("tax_id", observed=True)["y_sum_total"].first()
+    for t, v in g.items():
+        assert v == ysum[list(b.tax_id).index(int(t))]
+    # sort: N_alignments desc, then z = 1..15, -1..-15 within each taxon
+    first = df.groupby("tax_id", observed=True, sort=False).head(1)
+    assert (np.diff(first["N_alignments"].to_numpy().astype(np.int64)) <= 0).all()
+    assert (df["position"].to_numpy()[:30] == np.r_[np.arange(1, 16), -np.arange(1, 16)]).all()
+
+
+def test_load_counts_cache(tmp_path, ref_meta):
+    cfg = cfg_for(ref_meta["cases"]["data_ancient"], GOLDEN / "data_ancient.txt", out_dir=tmp_path)
+    df1 = counts.load_counts(cfg)
+    assert cfg.filename_counts.exists()
+    meta = __import__("metadamage_amd.io", fromlist=["Parquet"]).Parquet(cfg.filename_counts).load_metadata()
+    assert meta["shortname"] == cfg.shortname and meta["min_y_sum"] == 10
+    df2 = counts.load_counts(cfg)  # cache hit
+    assert len(df1) == len(df2) == 90
+    assert cfg.N_fits == 3
+
+
+def test_config_n_cores_rules():
+    avail = utils._cpu_count()
+    mk = lambda n: utils.Config(out_dir=".", max_fits=None, max_cores=n, min_alignments=10, min_y_sum=10,  # noqa
+                                substitution_bases_forward="CT", substitution_bases_reverse="GA",
+                                forced=False, version="0.0.0")
+    assert mk(1).N_cores == 1
+    assert mk(avail + 5).N_cores == avail - 1
+    assert mk(-2).N_cores == avail - 2
+
+
+def test_downcast_raises_on_uint32_overflow():
+    df = pd.DataFrame({"a": np.array([2**33], dtype=np.int64)})
+    with pytest.raises(AssertionError):
+        utils.downcast_dataframe(df, [])

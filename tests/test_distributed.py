@@ -1,0 +1,93 @@
+"""CPU tests of the multi-GPU path with the gloo backend (world size 2 and 3):
+contiguous taxon shards + the single gather of packed result records.  The
+per-shard fit is done by the CPU oracle here (a stand-in for the kernel; the
+GPU runs the same code path with the nccl/RCCL backend)."""
+
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from metadamage_amd.distributed import (REC_BYTES, alloc_records, gather_records, packed_views, shard_capacity,
+                                        shard_range, unpack_gathered)
+
+
+def test_shard_ranges_cover_in_order():
+    for T in (0, 1, 2, 7, 10, 10_001):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(T, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == T
+            for (a, b), (c, d) in zip(spans, spans[1:]):
+                assert b == c and a <= b
+            assert all(b - a <= shard_capacity(T, world) for a, b in spans)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, T, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from metadamage_amd.synthetic import generate
+        from oracle.oracle import OracleLib
+
+        b = generate(T, seed=8)
+        lo, hi = shard_range(T, rank, world)
+        cap = shard_capacity(T, world)
+        rec = alloc_records(cap, "cpu")
+        rec.zero_()
+        out, pred, status = packed_views(rec, cap)
+        if hi > lo:
+            o, p, s = OracleLib().fit_batch(b.y[lo:hi], b.N[lo:hi], b.mm[lo:hi], threads=1)
+            out[: hi - lo] = torch.from_numpy(o)
+            pred[: hi - lo] = torch.from_numpy(p)
+            status[: hi - lo] = torch.from_numpy(s)
+        parts = gather_records(rec, cap, rank, world)
+        if rank == 0:
+            q.put(unpack_gathered(parts, T, world))
+        else:
+            assert parts is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,T", [(2, 37), (3, 20), (2, 1)])
+def test_gloo_shard_and_gather_reproduce_single_process(world, T):
+    from metadamage_amd.synthetic import generate
+    from oracle.oracle import OracleLib
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, T, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    b = generate(T, seed=8)
+    o, pr, s = OracleLib().fit_batch(b.y, b.N, b.mm, threads=1)
+    assert got[0].shape == (T, 80)
+    np.testing.assert_array_equal(got[0], o)
+    np.testing.assert_array_equal(got[1], pr)
+    np.testing.assert_array_equal(got[2], s)
+
+
+def test_record_views_layout():
+    rec = alloc_records(5, "cpu")
+    out, pred, status = packed_views(rec, 5)
+    assert rec.numel() == 5 * REC_BYTES
+    assert out.shape == (5, 80) and pred.shape == (5, 3, 30) and status.shape == (5,)
+    assert out.is_contiguous() and pred.is_contiguous() and status.is_contiguous()
+    assert pred.data_ptr() - out.data_ptr() == 5 * 640

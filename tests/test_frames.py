@@ -1,0 +1,67 @@
+"""CPU tests of the output contract: fit_results / fit_predictions frames and
+their parquet files (column names, order, dtypes, "metadamage" metadata), built
+from oracle results (the GPU path produces the same arrays)."""
+
+from __future__ import annotations
+
+import numpy as np
+import pandas as pd
+
+from metadamage_amd import fits, io, utils
+from tests.helpers import GOLDEN
+
+
+def _cfg(tmp_path):
+    cfg = utils.Config(out_dir=tmp_path, max_fits=10, max_cores=1, min_alignments=10, min_y_sum=10,
+                       substitution_bases_forward="CT", substitution_bases_reverse="GA", forced=False,
+                       version="0.0.0")
+    cfg.add_filename(GOLDEN / "data_ancient.txt")
+    return cfg
+
+
+def _frames(tmp_path, oracle_lib):
+    cfg = _cfg(tmp_path)
+    df = pd.read_parquet(GOLDEN / "counts_data_ancient.parquet")
+    p = fits.pack_counts(df, cfg)
+    out, pred, st = oracle_lib.fit_batch(p.y, p.N, p.mm)
+    keep = st == 0
+    return cfg, p, out, pred, fits.make_df_fit_results(p, out, keep, cfg), fits.make_df_fit_predictions(p, pred, keep, cfg)
+
+
+def test_fit_results_columns_and_values(tmp_path, oracle_lib, ref_meta, ref_golden):
+    cfg, p, out, pred, dfr, dfp = _frames(tmp_path, oracle_lib)
+    assert list(dfr.columns) == ref_meta["fit_results_columns"]
+    assert list(dfp.columns) == ref_meta["fit_predictions_columns"]
+    assert list(dfr["tax_id"].astype(int)) == list(ref_golden["data_ancient__tax_id"])
+    assert (dfr["shortname"] == "data_ancient").all()
+    assert dfr["D_max"].dtype == np.float32 and dfr["N_alignments"].dtype == np.uint32
+    np.testing.assert_array_equal(dfr["D_max"].to_numpy(), out[:, 0].astype(np.float32))
+    np.testing.assert_array_equal(dfr["N_alignments"].to_numpy(), p.N_alignments.astype(np.uint32))
+    assert len(dfp) == 30 * len(dfr)
+    assert dfp["position"].dtype == np.int8
+    assert list(dfp["position"][:30]) == ref_meta["fit_predictions_position"]
+    np.testing.assert_array_equal(dfp["median"].to_numpy()[:30], pred[0, 0].astype(np.float32))
+
+
+def test_parquet_roundtrip_with_metadata(tmp_path, oracle_lib):
+    cfg, p, out, pred, dfr, dfp = _frames(tmp_path, oracle_lib)
+    pq = io.Parquet(cfg.filename_fit_results)
+    pq.save(dfr, metadata=cfg.to_dict())
+    meta = pq.load_metadata()
+    assert meta == cfg.to_dict()
+    assert set(meta) == {"out_dir", "max_fits", "max_cores", "min_alignments", "min_y_sum",
+                         "substitution_bases_forward", "substitution_bases_reverse", "forced", "version",
+                         "filename", "shortname", "N_filenames", "N_fits", "N_cores"}
+    back = pq.load()
+    assert list(back.columns) == list(dfr.columns)
+    assert isinstance(back["tax_id"].dtype, pd.CategoricalDtype)
+    assert pq.exists() and not pq.exists(forced=True)
+
+
+def test_failed_taxa_are_dropped(tmp_path, oracle_lib):
+    cfg, p, out, pred, _, _ = _frames(tmp_path, oracle_lib)
+    keep = np.array([True, False, True])
+    dfr = fits.make_df_fit_results(p, out, keep, cfg)
+    dfp = fits.make_df_fit_predictions(p, pred, keep, cfg)
+    assert list(dfr["tax_id"].astype(int)) == [int(p.tax_id[0]), int(p.tax_id[2])]
+    assert len(dfp) == 60
