@@ -1,0 +1,358 @@
+// mdfit_model.h — the per-point model, objective and Newton step shared by the
+// fit kernels of mdfit.hip (MDFIT-MAP v1).
+//
+// model_PMD / model_null log densities of /root/reference/metadamage/fits.py:43-67
+// (BetaBinomial log-pmf without the data-only log C(N,y)), their analytic
+// gradient and Hessian in the unconstrained coordinates
+// u = (logit q, logit A, c, log delta), and the projected, Hessian-modified
+// Newton direction.  Same formulas as oracle/mdfit_oracle.c (written separately).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/mdfit.h"
+#include "mdfit_special.h"
+
+namespace mdfit {
+
+constexpr int kNPos = MDFIT_NPOS;
+constexpr int kNHalf = MDFIT_NHALF;
+constexpr int kLD = MDFIT_LD;
+constexpr int kNMM = MDFIT_NMM;
+constexpr double kZ68 = 0.994457883209753;  // Phi^-1(0.84)
+
+// u = (logit q, logit A, c, log delta): c on its own scale (see oracle).
+__constant__ double kULo[4] = {-25.0, -25.0, 0.0, -25.0};
+__constant__ double kUHi[4] = {25.0, 25.0, 0.999, 20.0};
+constexpr double kEpsAct = 1e-8;
+constexpr double kNoiseF = 1.4e-14;  // objective rounding scale (oracle: NOISE_F)
+
+// ---------------------------------------------------------------------------
+// cross-lane sums inside aligned groups of G lanes (G = 2 ... 64)
+// ---------------------------------------------------------------------------
+// DPP move of a double (two 32-bit halves), all lanes active.
+template <int Ctrl>
+__device__ __forceinline__ double dpp(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), Ctrl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), Ctrl, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// Every step pairs lanes by an involution (quad_perm [1,0,3,2], [2,3,0,1],
+// row_half_mirror, row_mirror, then xor 16 / xor 32) and adds two
+// already-rounded values, so all G lanes end with bitwise-identical sums.  The
+// leading empty asm makes `v` opaque: without it hipcc (fp-contract=fast)
+// fuses the producer's multiply into the first add on THIS lane only
+// (fma(a, b, partner) vs the partner's rounded a*b) and the lanes of one group
+// drift apart in the last bit -- their Newton state machines then diverge.
+template <int G>
+__device__ __forceinline__ double gsum(double v) {
+  static_assert(G == 2 || G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "group size");
+  asm volatile("" : "+v"(v));
+  if (G >= 2) v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]  (xor 1)
+  if (G >= 4) v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]  (xor 2)
+  if (G >= 8) v += dpp<0x141>(v);  // row_half_mirror      (the other quad of the 8)
+  if (G >= 16) v += dpp<0x140>(v); // row_mirror           (the other 8 of the row)
+  if (G >= 32) v += __shfl_xor(v, 16, 64);
+  if (G >= 64) v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+__device__ __forceinline__ double clampd(double x, double lo, double hi) {
+  return fmin(fmax(x, lo), hi);
+}
+__device__ __forceinline__ double logit(double p) { return flog(p) - flog1p(-p); }
+
+// p = sigmoid(u), 1-p, ln p, ln(1-p) from one exp and one log1p
+__device__ __forceinline__ void logit_parts(double u, double& p, double& omp, double& lp,
+                                            double& l1mp) {
+  const double e = exp(-fabs(u));
+  const double r = rcp(1.0 + e);
+  const double sp = flog1p(e);
+  const bool pos = u >= 0.0;
+  p = pos ? r : e * r;
+  omp = pos ? e * r : r;
+  lp = pos ? -sp : u - sp;
+  l1mp = pos ? -(u + sp) : -sp;
+}
+
+// Constrained parameters of one trial point u (group-uniform), computed once
+// per trial instead of once per point evaluation; kept lean (registers).
+struct Theta {
+  double q, omq, iomq;        // q, 1-q, 1/(1-q)
+  double A, JA;               // A and A(1-A) (PMD only)
+  double c, iomc;             // c and 1/(1-c) (PMD only; c on its own scale)
+  double delta, phi;
+  double lprior;              // log prior at u (constants dropped)
+};
+
+__device__ __forceinline__ Theta make_theta(bool pmd, const double u[4]) {
+  Theta th;
+  double lq, l1mq;
+  logit_parts(u[0], th.q, th.omq, lq, l1mq);
+  th.iomq = rcp(th.omq);
+  th.delta = exp(u[3]);
+  th.phi = th.delta + 2.0;
+  // ln q + 2 ln(1-q) - delta/1000  [+ ln A + 2 ln(1-A) + 8 ln(1-c)]  (fits.py:46-53)
+  th.lprior = lq + 2.0 * l1mq - th.delta / 1000.0;
+  if (pmd) {
+    double omA, lA, l1mA;
+    logit_parts(u[1], th.A, omA, lA, l1mA);
+    th.JA = th.A * omA;
+    th.c = u[2];
+    th.iomc = rcp(1.0 - th.c);
+    th.lprior += lA + 2.0 * l1mA + 8.0 * flog1p(-th.c);
+  } else {
+    th.A = th.JA = th.c = 0.0;
+    th.iomc = 1.0;
+  }
+  return th;
+}
+
+// theta-space sums of one objective evaluation (before the chain rule):
+// 0 ell, 1 mag, 2..5 G(q,A,c,phi), 6..15 H upper triangle
+// (qq qA qc qphi AA Ac Aphi cc cphi phiphi)
+constexpr int kNAcc = 16;
+
+// x^k for 0 <= k < 16 by binary powering (3 squarings, 3 products): cheaper
+// than exp(k ln x) and as accurate (a few rounding errors).
+__device__ __forceinline__ double powk(double x, int k) {
+  const double x2 = x * x, x4 = x2 * x2, x8 = x4 * x4;
+  const double a = (k & 1) ? x : 1.0, b = (k & 2) ? x2 : 1.0;
+  const double c = (k & 4) ? x4 : 1.0, d = (k & 8) ? x8 : 1.0;
+  return (a * b) * (c * d);
+}
+
+// Per-lane point data of the current phase.
+struct PointData {
+  double y, N;
+  int k;       // |z| - 1
+  bool valid;  // a real point (not a pad lane)
+  bool pmd;    // lane group fits model_PMD (else model_null)
+};
+
+// One point's contribution at theta, ADDED to acc (same formulas as
+// oracle/mdfit_oracle.c evaluate(); derivation in DESIGN.md §3).  Returns the
+// point's log-likelihood (without log C(N,y)).
+__device__ __forceinline__ double point_accum(const PointData& pd, const Theta& th,
+                                              double acc[kNAcc]) {
+  double D, Dq, DA, Dc, Dqq, DqA;
+  if (pd.pmd) {
+    const double kk = (double)pd.k;
+    const double w = powk(th.omq, pd.k);  // (1-q)^k
+    const double wq = w * th.iomq;        // (1-q)^(k-1)
+    D = fma(th.A, w, th.c);
+    DA = w;
+    Dc = 1.0;
+    Dq = pd.k >= 1 ? -th.A * kk * wq : 0.0;
+    DqA = pd.k >= 1 ? -kk * wq : 0.0;
+    Dqq = pd.k >= 2 ? th.A * kk * (kk - 1.0) * (wq * th.iomq) : 0.0;
+  } else {
+    D = th.q;
+    Dq = 1.0;
+    DA = Dc = Dqq = DqA = 0.0;
+  }
+  const double phi = th.phi;
+  const double omD = 1.0 - D;
+  const double a = D * phi, b = omD * phi;
+  // paired so that each pair's lnGamma / psi / psi1 difference is formed as
+  // soon as both halves exist (fewer live registers)
+  const LG3 t1 = lg3(pd.y + a);
+  const LG3 t4 = lg3(a);
+  const double la = t1.l - t4.l, Pa = t1.p - t4.p, Qa = t1.q - t4.q;
+  double mag = fabs(t1.l) + fabs(t4.l);
+  const LG3 t2 = lg3(pd.N - pd.y + b);
+  const LG3 t5 = lg3(b);
+  const double lb = t2.l - t5.l, Pb = t2.p - t5.p, Qb = t2.q - t5.q;
+  mag += fabs(t2.l) + fabs(t5.l);
+  const LG3 t3 = lg3(pd.N + phi);
+  const LG3 t6 = lg3(phi);
+  const double lS = t3.l - t6.l, S = t6.p - t3.p, S1 = t6.q - t3.q;
+  mag += fabs(t3.l) + fabs(t6.l);
+  const double ell = (la + lb) - lS;  // exact 0 when N = 0
+  const double lD = phi * (Pa - Pb);
+  const double lF = D * Pa + omD * Pb + S;
+  const double lDD = phi * phi * (Qa + Qb);
+  const double lDF = (Pa - Pb) + phi * (D * Qa - omD * Qb);
+  const double lFF = D * D * Qa + omD * omD * Qb + S1;
+  if (pd.valid) {
+    acc[0] += ell;
+    acc[1] += mag;
+    acc[2] += lD * Dq;
+    acc[3] += lD * DA;
+    acc[4] += lD * Dc;
+    acc[5] += lF;
+    acc[6] += lDD * Dq * Dq + lD * Dqq;
+    acc[7] += lDD * Dq * DA + lD * DqA;
+    acc[8] += lDD * Dq * Dc;
+    acc[9] += lDF * Dq;
+    acc[10] += lDD * DA * DA;
+    acc[11] += lDD * DA * Dc;
+    acc[12] += lDF * DA;
+    acc[13] += lDD * Dc * Dc;
+    acc[14] += lDF * Dc;
+    acc[15] += lFF;
+  }
+  return ell;
+}
+
+// Value-only log-likelihood of one point (lnGamma only; the record assembly
+// needs the pointwise log-likelihoods at the modes).
+__device__ __forceinline__ double point_ell(double y, double N, double D, double phi) {
+  const double a = D * phi, b = (1.0 - D) * phi;
+  const double la = lg3(y + a).l - lg3(a).l;
+  const double lb = lg3(N - y + b).l - lg3(b).l;
+  const double lS = lg3(N + phi).l - lg3(phi).l;
+  return (la + lb) - lS;
+}
+
+// Objective in u-space from the group sums (oracle: evaluate(), chain rule
+// part).  H is the packed upper triangle in acc order: qq qA qc qphi AA Ac
+// Aphi cc cphi phiphi.
+struct Eval {
+  double F, mag;
+  double g[4];
+  double H[10];
+};
+
+__device__ __forceinline__ int hidx(int j, int m) {  // packed index, j <= m
+  return j == 0 ? m : (j == 1 ? 3 + m : (j == 2 ? 5 + m : 9));
+}
+
+__device__ __forceinline__ void finish_eval(bool pmd, const Theta& th, const double s[kNAcc],
+                                            Eval& e) {
+  const double q = th.q, A = th.A, c = th.c, delta = th.delta;
+  const double J[4] = {q * th.omq, th.JA, 1.0, delta};
+  const double J2[4] = {J[0] * (1.0 - 2.0 * q), th.JA * (1.0 - 2.0 * A), 0.0, delta};
+  const double gp[4] = {1.0 - 3.0 * q, pmd ? 1.0 - 3.0 * A : 0.0, pmd ? -8.0 * th.iomc : 0.0,
+                        -delta / 1000.0};
+  const double hp[4] = {-3.0 * J[0], pmd ? -3.0 * th.JA : 0.0,
+                        pmd ? -8.0 * th.iomc * th.iomc : 0.0, -delta / 1000.0};
+  const bool infeasible = pmd && (A + c >= 1.0);
+  e.F = infeasible ? INFINITY : -(s[0] + th.lprior);
+  e.mag = s[1];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool fixed = !pmd && (j == 1 || j == 2);
+    e.g[j] = fixed ? 0.0 : -(J[j] * s[2 + j] + gp[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int m = j; m < 4; ++m) {
+      const int k = hidx(j, m);
+      double h = J[j] * s[6 + k] * J[m];
+      if (j == m) h += J2[j] * s[2 + j] + hp[j];
+      const bool fixed = !pmd && (j == 1 || j == 2 || m == 1 || m == 2);
+      e.H[k] = fixed ? 0.0 : -h;
+    }
+  }
+}
+
+__device__ __forceinline__ double maxabs4(const double v[4]) {
+  return fmax(fmax(fabs(v[0]), fabs(v[1])), fmax(fabs(v[2]), fabs(v[3])));
+}
+
+// projected-gradient size (oracle: pgnorm): 0 for a variable held on its bound
+__device__ __forceinline__ double pgnorm(const double u[4], const double g[4]) {
+  double m = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) m = fmax(m, fabs(u[j] - clampd(u[j] - g[j], kULo[j], kUHi[j])));
+  return m;
+}
+
+__constant__ double kEpsBind[4] = {1e-3, 1e-3, 1e-4, 1e-3};
+
+// Cholesky of the free block of H + mu*I (fixed / bound rows -> identity);
+// false if a pivot is not positive.  Packed lower triangle L (same index as
+// H), iL = 1 / diag(L).
+__device__ __forceinline__ bool chol4(const bool fr[4], const double H[10], double mu, double L[10],
+                                      double iL[4]) {
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+#pragma unroll
+    for (int m = 0; m <= j; ++m) {
+      double s;
+      if (!fr[j] || !fr[m]) s = (j == m) ? 1.0 : 0.0;
+      else s = H[hidx(m, j)] + ((j == m) ? mu : 0.0);
+#pragma unroll
+      for (int p = 0; p < m; ++p) s -= L[hidx(p, j)] * L[hidx(p, m)];
+      if (j == m) {
+        if (!(s > 0.0)) ok = false;
+        const double lj = sqrt(fmax(s, 1e-300));
+        L[hidx(j, j)] = lj;
+        iL[j] = rcp(lj);
+      } else {
+        L[hidx(m, j)] = s * iL[m];  // L(j,m) stored at packed (m,j)
+      }
+    }
+  }
+  return ok;
+}
+
+// Projected, Hessian-modified Newton direction with a Bertsekas binding set
+// (oracle: direction()): variables within eps of a bound and pushed outward
+// step onto the bound and leave the Newton system.
+__device__ __forceinline__ void newton_dir(bool pmd, const double u[4], const double g[4],
+                                           const double H[10], double d[4]) {
+  bool fr[4];
+  double dbind[4];
+  double w = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool fixed = !pmd && (j == 1 || j == 2);
+    if (!fixed) w = fmax(w, fabs(u[j] - clampd(u[j] - g[j], kULo[j], kUHi[j])));
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool fixed = !pmd && (j == 1 || j == 2);
+    const double eps = fmin(kEpsBind[j], w);
+    const bool atlo = u[j] - kULo[j] <= eps, athi = kUHi[j] - u[j] <= eps;
+    // on / next to a box bound and not pulled inward by more than kEpsAct
+    const bool bind = (atlo && g[j] > -kEpsAct) || (athi && g[j] < kEpsAct);
+    dbind[j] = (bind && !fixed) ? (atlo ? kULo[j] : kUHi[j]) - u[j] : 0.0;
+    fr[j] = !(fixed || bind);
+  }
+  double L[10], iL[4];
+  bool ok = chol4(fr, H, 0.0, L, iL);  // plain Newton: the common case
+  if (!ok) {  // indefinite: shift the diagonal by 1e-10 * scale, x10 per retry
+    double sc = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (fr[j]) sc = fmax(sc, fabs(H[hidx(j, j)]));
+    if (sc == 0.0) sc = 1.0;
+    double mu = 1e-10 * sc;
+    for (int attempt = 1; attempt < 40 && !ok; ++attempt, mu *= 10.0) ok = chol4(fr, H, mu, L, iL);
+  }
+  if (!ok) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d[j] = (fr[j] && isfinite(g[j])) ? -g[j] : 0.0;
+  } else {
+    double z[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // L z = -g (free rows)
+      double s = fr[j] ? -g[j] : 0.0;
+#pragma unroll
+      for (int p = 0; p < j; ++p) s -= L[hidx(p, j)] * z[p];
+      z[j] = s * iL[j];
+    }
+#pragma unroll
+    for (int j = 3; j >= 0; --j) {  // L^T d = z
+      double s = z[j];
+#pragma unroll
+      for (int p = j + 1; p < 4; ++p) s -= L[hidx(j, p)] * d[p];
+      d[j] = s * iL[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (!fr[j]) d[j] = dbind[j];
+  const double mx = maxabs4(d);
+  if (mx > 4.0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d[j] *= 4.0 / mx;
+  }
+}
+
+}  // namespace mdfit

@@ -3,7 +3,9 @@
 // The fit needs, per beta-binomial point and per objective evaluation, the
 // triple (lnGamma, psi, psi1) at six arguments (y+a, a, N-y+b, b, N+phi, phi).
 // One call here returns all three from ONE log and ONE reciprocal of the
-// (possibly shifted) argument:
+// (possibly shifted) argument (both hand-rolled below: the library log is a
+// double-double routine ~3x longer, and the IEEE divide sequence is not
+// needed where the result feeds a series):
 //
 //   x < 10:  shift by 10 with the product P(x) = prod_{j<10} (x+j) and its
 //            first two derivatives (P'/P = sum 1/(x+j),
@@ -17,6 +19,51 @@
 #include <hip/hip_runtime.h>
 
 namespace mdfit {
+
+// FP64 reciprocal: v_rcp_f64 + two Newton steps (faithful, no IEEE div sequence)
+__device__ __forceinline__ double rcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(fma(-x, r, 1.0), r, r);
+  r = fma(fma(-x, r, 1.0), r, r);
+  return r;
+}
+
+// Natural log, <= ~1 ulp (the classic reduction x = 2^e (1+f), 1+f in
+// [sqrt(1/2), sqrt(2)), log(1+f) = f - hfsq + s (hfsq + R(s^2)), s = f/(2+f),
+// R a degree-7 minimax polynomial in s^2 -- Cody & Waite / the fdlibm scheme).
+// 0 -> -inf, +inf -> +inf, negative / NaN -> NaN.
+__device__ __forceinline__ double flog(double x) {
+  constexpr double kLn2Hi = 6.93147180369123816490e-01;  // high 32 bits of ln 2
+  constexpr double kLn2Lo = 1.90821492927058770002e-10;  // ln 2 - kLn2Hi
+  constexpr double kSqrtHalf = 0.70710678118654752440;
+  double m = __builtin_amdgcn_frexp_mant(x);  // [0.5, 1)
+  int e = __builtin_amdgcn_frexp_exp(x);
+  const bool lo = m < kSqrtHalf;
+  m = lo ? m + m : m;
+  e = lo ? e - 1 : e;
+  const double f = m - 1.0;  // exact
+  const double s = f * rcp(2.0 + f);
+  const double z = s * s, w = z * z;
+  const double t1 = w * fma(w, fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01),
+                            3.999999999940941908e-01);
+  const double t2 =
+      z * fma(w, fma(w, fma(w, 1.479819860511658591e-01, 1.818357216161805012e-01),
+                     2.857142874366239149e-01),
+              6.666666666666735130e-01);
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  const double de = (double)e;
+  const double r = de * kLn2Hi - ((hfsq - fma(s, hfsq + R, de * kLn2Lo)) - f);
+  const bool normal = x > 0.0 && x < INFINITY;
+  return normal ? r : (x == 0.0 ? -INFINITY : (x == INFINITY ? x : NAN));
+}
+
+// log(1 + x), x > -1: Goldberg's correction log(u) * x / (u - 1), u = 1 + x.
+__device__ __forceinline__ double flog1p(double x) {
+  const double u = 1.0 + x;
+  const double um1 = u - 1.0;
+  return um1 == 0.0 ? x : flog(u) * (x * rcp(um1));
+}
 
 struct LG3 {
   double l;  // lnGamma(x)
@@ -39,9 +86,9 @@ __device__ __forceinline__ LG3 lg3(double x) {
     }
     xs = x + 10.0;
   }
-  const double r = 1.0 / xs;
+  const double r = rcp(xs);
   const double r2 = r * r;
-  const double lx = log(xs);
+  const double lx = flog(xs);
   // lnGamma(xs) ~ (xs - 1/2) ln xs - xs + ln(2 pi)/2 + r (1/12 - r2 (1/360 - ...))
   double sl = fma(r2, -1.0 / 156.0, 691.0 / 360360.0);
   sl = fma(r2, -sl, 1.0 / 1188.0);
@@ -67,10 +114,10 @@ __device__ __forceinline__ LG3 lg3(double x) {
   sq = fma(r2, -sq, 1.0 / 6.0);
   double Q = r + 0.5 * r2 + r * r2 * sq;
   if (shift) {
-    const double iP = 1.0 / P;
+    const double iP = rcp(P);
     const double s1 = dP * iP;          // sum 1/(x+j)
     const double s2 = s1 * s1 - d2P * iP;  // sum 1/(x+j)^2
-    L -= log(P);
+    L -= flog(P);
     Ps -= s1;
     Q += s2;
   }

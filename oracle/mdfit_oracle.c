@@ -403,11 +403,13 @@ typedef struct {
 static int g_trace = 0; /* debugging aid: print every evaluation of fit_one */
 void oracle_set_trace(int on) { g_trace = on; }
 
+/* u0 == NULL: the data-driven initial point (init_u); else start at u0 */
 static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
-                    int hi, int max_iter, double tol, fitres* out) {
+                    int hi, int max_iter, double tol, const double* u0, fitres* out) {
   double u[4], d[4], ut[4], t = 1.0;
   evalres cur, tr;
-  init_u(model, y, N, lo, hi, u);
+  if (u0) memcpy(u, u0, sizeof(u));
+  else init_u(model, y, N, lo, hi, u);
   evaluate(model, y, N, lo, hi, u, &cur);
   int evals = 1, status = MDFIT_MAXITER;
   if (!isfinite(cur.F)) {
@@ -567,7 +569,14 @@ static void fit_taxon(const uint32_t* y, const uint32_t* N, const uint32_t* mm,
   fitres f[6];
   int st = MDFIT_OK;
   for (int s = 0; s < 6; s++) {
-    fit_one(models[s], y, N, los[s], his[s], o->max_iter, o->tol_step, &f[s]);
+    /* MDFIT-MAP v1 warm start: the forward / reverse sub-fits start from the
+     * all-position mode of the same model when that fit converged */
+    const double* u0 = NULL;
+    if (s >= 2) {
+      const fitres* base = &f[models[s] == M_PMD ? 0 : 1];
+      if (base->status == MDFIT_OK) u0 = base->u;
+    }
+    fit_one(models[s], y, N, los[s], his[s], o->max_iter, o->tol_step, u0, &f[s]);
     if (f[s].status > st) st = f[s].status;
     double* dg = out + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * s;
     dg[0] = sigm(f[s].u[P_Q]);
@@ -683,13 +692,13 @@ void oracle_objective(int model, int subset, const uint32_t* y, const uint32_t* 
     for (int i = 0; i < NPOS; i++) ell30[i] = (i >= lo && i < hi) ? r.ell[i] : 0.0;
 }
 
-/* One sub-fit from the spec's initial point; returns u*, F*, evals, status. */
+/* One sub-fit from u0 (NULL: the spec's initial point); returns u*, F*, evals, status. */
 void oracle_fit_subfit(int model, int subset, const uint32_t* y, const uint32_t* N,
-                       int max_iter, double tol, double* u4, double* F,
+                       int max_iter, double tol, const double* u0, double* u4, double* F,
                        int32_t* evals, int32_t* status) {
   int lo = subset == 2 ? NHALF : 0, hi = subset == 1 ? NHALF : NPOS;
   fitres f;
-  fit_one(model, y, N, lo, hi, max_iter, tol, &f);
+  fit_one(model, y, N, lo, hi, max_iter, tol, u0, &f);
   for (int j = 0; j < 4; j++) u4[j] = f.u[j];
   *F = f.r.F;
   *evals = f.evals;

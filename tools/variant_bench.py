@@ -1,0 +1,70 @@
+"""Time mdfit_fit_batch of several builds of the engine on the same batch
+(development tool: kernel-design A/B at the bench workload).
+
+    python tools/variant_bench.py metadamage_amd/libmdfit_A.so metadamage_amd/libmdfit_B.so
+"""
+
+from __future__ import annotations
+
+import argparse
+import ctypes
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--taxa", type=int, default=10_000)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--reps", type=int, default=2)
+    a = ap.parse_args()
+
+    import torch
+
+    from metadamage_amd import _lib, engine
+    from metadamage_amd.synthetic import generate
+
+    b = generate(a.taxa, seed=1)
+    ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm)
+    o = _lib.default_opts()
+    libs = [(p, _lib.load(p)) for p in a.libs]
+    ref = None
+    for rep in range(a.reps):
+        for path, lib in libs:
+            res = engine.alloc_outputs(a.taxa)
+
+            def call():
+                _lib.check(lib.mdfit_fit_batch(
+                    ctypes.c_void_p(ty.data_ptr()), ctypes.c_void_p(tN.data_ptr()),
+                    ctypes.c_void_p(tm.data_ptr()), a.taxa, ctypes.byref(o),
+                    ctypes.c_void_p(res.out.data_ptr()), ctypes.c_void_p(res.pred.data_ptr()),
+                    ctypes.c_void_p(res.status.data_ptr()), ctypes.c_void_p(res.workspace.data_ptr()),
+                    ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+
+            for _ in range(3):
+                call()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.steps):
+                call()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / a.steps
+            out = res.out.cpu().numpy()[:, :25]
+            st = res.status.cpu().numpy()
+            if ref is None:
+                ref = out
+            dev = np.nanmax(np.abs(out - ref) / (np.abs(ref) + 1e-300)) if ref is not None else 0.0
+            print(f"rep {rep} {Path(path).name:24s} {ms:8.3f} ms  {a.taxa / ms * 1e3 / 1e6:6.2f} M fits/s  "
+                  f"ok {np.mean(st == 0):.4f}  max rel dev vs first {dev:.1e}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
