@@ -127,7 +127,7 @@ void mdfit_default_opts(mdfit_opts* opts);
  *   out       : double[n_taxa][MDFIT_NOUT]                  (device)
  *   pred      : float[n_taxa][MDFIT_NPRED][MDFIT_NPOS] or NULL (device)
  *   status    : int32_t[n_taxa]                             (device)
- *   workspace : device buffer of mdfit_workspace_bytes() bytes (work-queue counter)
+ *   workspace : device buffer of mdfit_workspace_bytes(n_taxa) bytes (work queues)
  *   hip_stream: hipStream_t or NULL
  * Replaces compute_fits' per-taxon loop (fits.py:477-526, 569-626, 709-730).
  */
@@ -136,8 +136,8 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm,
                     float* pred, int32_t* status, void* workspace,
                     void* hip_stream);
 
-/* Bytes of device workspace mdfit_fit_batch needs. */
-int64_t mdfit_workspace_bytes(void);
+/* Bytes of device workspace mdfit_fit_batch needs for n_taxa taxa. */
+int64_t mdfit_workspace_bytes(int64_t n_taxa);
 
 /*
  * Pointwise beta-binomial log-pmf (numpyro BetaBinomial.log_prob, used by

@@ -109,7 +109,7 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.mdfit_default_opts.restype = None
     lib.mdfit_fit_batch.argtypes = [vp, vp, vp, i64, ctypes.POINTER(MdfitOpts), vp, vp, vp, vp, vp]
     lib.mdfit_fit_batch.restype = ctypes.c_int
-    lib.mdfit_workspace_bytes.argtypes = []
+    lib.mdfit_workspace_bytes.argtypes = [i64]
     lib.mdfit_workspace_bytes.restype = i64
     lib.mdfit_betabinom_logpmf.argtypes = [vp, vp, vp, vp, i64, vp, vp, vp]
     lib.mdfit_betabinom_logpmf.restype = ctypes.c_int

@@ -2,27 +2,33 @@
 //
 // Replaces the per-taxon NUTS loop of /root/reference/metadamage/fits.py
 // (compute_fits :709-730 -> fit_single_group_without_timeout :428-469) with
-// three stream-ordered launches over a dense count tensor (MDFIT-MAP v1,
+// four stream-ordered launches over a dense count tensor (MDFIT-MAP v1,
 // DESIGN.md §3-4):
 //
-//   K1 fit_tasks_kernel<kAll>  2T sub-fits: model_PMD and model_null on all 30
-//                              positions (fits.py:438-439)
-//   K2 fit_tasks_kernel<kFR>   4T sub-fits: PMD / null on z>0 and z<0
-//                              (fits.py:311-313, 333-335), warm-started at the
-//                              K1 modes
-//   K3 assemble_kernel         one wave per taxon: pointwise log-likelihoods at
+//   K0 init_kernel     the data-driven initial point of all 6T sub-fits
+//   K1 fit_kernel      persistent: first the 2T all-position sub-fits
+//                      (model_PMD / model_null, fits.py:438-439), then the 4T
+//                      forward / reverse ones (fits.py:311-313, 333-335),
+//                      warm-started at the all-position modes
+//   K3 assemble_kernel one wave per taxon: pointwise log-likelihoods at
 //                              the 6 modes, n_sigma x3, asymmetry, predictive
 //                              summaries, sums, noise (fits.py:230-376)
 //
-// K1/K2 work decomposition: one sub-fit = one group of G aligned lanes (8 for
-// the 30-position fits, 4 for the 15-position ones), every lane owning 4
-// position slots, so a wave runs 8 or 16 independent Newton state machines.
-// Per trip each group evaluates value + gradient + Hessian at its trial point
-// (4 point evaluations per lane, then a 3- or 2-step DPP butterfly), and runs
-// its Newton logic.  A group whose fit has converged pulls the next sub-fit
-// from a work queue (one atomic per wave-trip, 8 queues = one per XCD), so no
-// lane waits for the slowest fit of its wave.  Everything is FP64 (the
-// reference enables x64, fits.py:32).
+// K1 work decomposition: a wave = 2 groups of 32 lanes, a group = 2 halves of
+// 16 lanes, lane = position (half 0: z = 1..15, half 1: z = -1..-15, lane 15
+// of a half is a pad).  A group runs either one all-position sub-fit (the
+// halves' sums added: both hold identical Newton state) or the forward /
+// reverse pair of one model (each half its own Newton state machine).  Per
+// trip every running fit evaluates value + gradient + Hessian at its trial
+// point (one point per lane, then a DPP butterfly) and runs its Newton logic.
+// Free groups pull all-position tasks from 8 per-XCD queues (one atomic per
+// wave-trip); once those are drained they take fwd/rev pairs from a ready
+// ring that each finished all-position fit appends its pair to (release /
+// acquire at agent scope: the pair's warm-start u0 is in the record), so the
+// pairs of early taxa run while the last all-position fits are still going.
+// (Claiming one task ahead to hide the atomic + load latency was measured
+// slower: the last tasks then queue behind long fits while other groups sit
+// idle.)  Everything is FP64 (the reference enables x64, fits.py:32).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -38,16 +44,17 @@ namespace mdfit {
 
 constexpr int kWave = 64;
 constexpr int kQueues = 8;      // one work queue per XCD (blockIdx % 8 share an XCD)
-#ifndef MDFIT_LANES_ALL
-#define MDFIT_LANES_ALL 32
-#endif
-constexpr int kLanesAll = MDFIT_LANES_ALL;  // lanes per 30-position sub-fit (32/G slots each)
 constexpr int kAll = 0, kFR = 1;
 
 // diag slots of the out record (include/mdfit.h): during K1/K2 slots 0..3 of a
 // sub-fit hold its unconstrained mode u*, K3 turns them into (q, A, c, phi)
 __device__ __forceinline__ double* diag(double* out, int64_t taxon, int sub) {
   return out + taxon * MDFIT_NOUT + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * sub;
+}
+
+// v[j] for a lane-varying j in 0..3 without dynamic register indexing
+__device__ __forceinline__ double sel4(const double v[4], int j) {
+  return j == 0 ? v[0] : (j == 1 ? v[1] : (j == 2 ? v[2] : v[3]));
 }
 
 #ifdef MDFIT_STAMP
@@ -63,49 +70,99 @@ __device__ __forceinline__ unsigned long long stamp() {
 #endif
 
 // ---------------------------------------------------------------------------
-// K1 / K2: persistent sub-fit kernels
+// K0: initial points (oracle: init_u)
 // ---------------------------------------------------------------------------
-// Position slot i of lane-in-group r: slot p = r + G*i holds all-position
-// column p (|z|-1 = p mod 15) for kAll, half-column p for kFR; y, N unset.
-template <int KIND>
-__device__ __forceinline__ PointData slot_point(int r, int i, bool pmd) {
-  constexpr int G = KIND == kAll ? kLanesAll : kLanesAll / 2;
-  const int p = r + G * i;
-  PointData pd;
-  pd.pmd = pmd;
-  pd.valid = p < (KIND == kAll ? kNPos : kNHalf);
-  pd.k = pd.valid ? (KIND == kAll ? (p < kNHalf ? p : p - kNHalf) : p) : 0;
-  pd.y = pd.N = 0.0;
-  return pd;
+// |z|-1 of all-position column i (0..14 forward, 15..29 reverse)
+__device__ __forceinline__ int kpos(int i) { return i < kNHalf ? i : i - kNHalf; }
+
+// One thread per (taxon, sub-fit): pooled ratios over the sub-fit's positions
+// -> u0 in diag slots 0..3 (K1 / K2 start there; K1 replaces the fwd/rev u0
+// by its own mode when it converged -- the warm start).
+__global__ __launch_bounds__(256) void init_kernel(const uint32_t* __restrict__ gy,
+                                                   const uint32_t* __restrict__ gN, int64_t T,
+                                                   double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= MDFIT_NSUBFIT * T) return;
+  const int64_t taxon = i / MDFIT_NSUBFIT;
+  const int sub = (int)(i % MDFIT_NSUBFIT);  // 0 PMD-all 1 null-all 2 PMD-f 3 PMD-r 4 null-f 5 null-r
+  const bool pmd = sub == 0 || sub == 2 || sub == 3;
+  const int lo = (sub == 3 || sub == 5) ? kNHalf : 0;
+  const int hi = sub < 2 ? kNPos : lo + kNHalf;
+  double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // y,N over all, |z|=1, |z|=2, |z|>=10
+  for (int c = lo; c < hi; ++c) {
+    const double y = (double)gy[taxon * kLD + c], N = (double)gN[taxon * kLD + c];
+    const int k = kpos(c);
+    s[0] += y;
+    s[1] += N;
+    if (k == 0) { s[2] += y; s[3] += N; }
+    if (k == 1) { s[4] += y; s[5] += N; }
+    if (k >= 9) { s[6] += y; s[7] += N; }
+  }
+  double u0[4];
+  u0[3] = flog(100.0);
+  if (!pmd) {
+    u0[0] = logit(clampd((s[0] + 0.5) / (s[1] + 1.0), 1e-4, 0.9));
+    u0[1] = u0[2] = 0.0;
+  } else {
+    const double c0 = clampd((s[6] + 0.5) / (s[7] + 1.0), 1e-4, 0.3);
+    const double r1 = (s[2] + 0.5) / (s[3] + 1.0);
+    const double r2 = (s[4] + 0.5) / (s[5] + 1.0);
+    const double A0 = clampd(r1 - c0, 1e-3, 0.9 * (1.0 - c0));
+    double q0 = 1.0 / 3.0;
+    if (r1 - c0 > 1e-3) q0 = clampd(1.0 - (r2 - c0) / (r1 - c0), 0.05, 0.95);
+    u0[0] = logit(q0);
+    u0[1] = logit(A0);
+    u0[2] = c0;
+  }
+  double* dg = diag(out, taxon, sub);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dg[j] = u0[j];
 }
 
+// ---------------------------------------------------------------------------
+// K1: the persistent fit kernel (all 6 sub-fits of every taxon)
+// ---------------------------------------------------------------------------
 #ifndef MDFIT_FIT_WAVES_PER_EU
 #define MDFIT_FIT_WAVES_PER_EU 2
 #endif
 
-template <int KIND>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_FIT_WAVES_PER_EU)))
-void fit_tasks_kernel(
-    const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN, int64_t T, int max_iter,
-    double tol, double* __restrict__ out, int* __restrict__ queue) {
-  constexpr int G = KIND == kAll ? kLanesAll : kLanesAll / 2;  // lanes per sub-fit
-  constexpr int SLOTS = KIND == kAll ? 32 : 16;                 // position slots
-  constexpr int P = SLOTS / G;                                  // slots per lane
-  const int lane = threadIdx.x;
-  const int r = lane % G;
-  const int leader = lane - r;
-  const int64_t ntask = (KIND == kAll ? 2 : 4) * T;
-  const int qi = blockIdx.x % kQueues;
-  const int64_t qlo = ntask * qi / kQueues, qhi = ntask * (qi + 1) / kQueues;
-  int* ctr = queue + KIND * kQueues + qi;
+// workspace layout (int32): [0, 8) per-XCD all-position task counters,
+// [8] ring push counter, [9] ring pop counter, [16, 16 + 2T) ready ring
+constexpr int kWsPush = 8, kWsPop = 9, kWsRing = 16;
 
-  // group state (replicated on the group's lanes)
+// group modes
+constexpr int kIdle = 0, kAllFit = 1, kPairFit = 2, kWaitRing = 3;
+
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_FIT_WAVES_PER_EU)))
+void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN, int64_t T,
+                int max_iter, double tol, double* __restrict__ out, int* __restrict__ ws) {
+  const int lane = threadIdx.x;
+  const int r = lane & 31;       // lane in the 32-lane group
+  const int h = r >> 4;          // half: 0 forward (z > 0), 1 reverse (z < 0)
+  const int leader = lane & ~31;
+  const int qi = blockIdx.x % kQueues;
+  const int64_t nall = 2 * T;  // all-position tasks: (taxon, model)
+  const int64_t qlo = nall * qi / kQueues, qhi = nall * (qi + 1) / kQueues;
+  int* ring = ws + kWsRing;
+
+  // this lane's position: column h*15 + i, |z|-1 = i (lane i = 15 of a half is a pad)
+  PointData pd;
+  {
+    const int i = r & 15;
+    pd.valid = i < kNHalf;
+    pd.k = pd.valid ? i : 0;
+  }
+  const int col = pd.valid ? h * kNHalf + pd.k : 0;
+  pd.y = pd.N = 0.0;
+  pd.pmd = true;
+
+  int mode = kIdle, slot = 0;
+  bool all_drained = false, ring_drained = false;
+  // the sub-fit of this lane's half (replicated on its 16 lanes; for an
+  // all-position fit both halves hold identical state)
   int64_t taxon = 0;
   int sub = 0;
-  bool pmd = true, active = false, exhausted = false;
-  // per-lane point data of the current sub-fit in LDS, [slot][lane] (no
-  // dynamically indexed register arrays -> no scratch)
-  __shared__ double s_py[P][kWave], s_pN[P][kWave];
+  bool running = false;
   double u[4] = {0, 0, 0, 0}, ut[4] = {0, 0, 0, 0}, d[4] = {0, 0, 0, 0};
   Theta th = make_theta(true, u);
   double curF = INFINITY, curMag = 0.0, curPg = 0.0, t = 1.0;
@@ -120,117 +177,103 @@ void fit_tasks_kernel(
 #ifdef MDFIT_STAMP
     const unsigned long long f0 = stamp();
 #endif
-    // ---- 1. groups without a sub-fit pull one (one atomic per wave-trip) ----
     bool starting = false;
-    const bool need = !active && !exhausted;
-    const unsigned long long m = __ballot(need && r == 0);
-    if (m != 0ull) {
+    // ---- 1. idle groups pull an all-position task (one atomic per wave-trip) --
+    const bool need1 = mode == kIdle && !all_drained;
+    if (__any(need1)) {
+      const unsigned long long m = __ballot(need1 && r == 0);
       int base = 0;
-      if (lane == 0) base = atomicAdd(ctr, __popcll(m));
+      if (lane == 0) base = atomicAdd(ws + qi, __popcll(m));
       base = __shfl(base, 0);
-      if (need) {
-        const int rank = __popcll(m & ((1ull << leader) - 1ull));
-        const int64_t task = qlo + base + rank;
+      if (need1) {
+        const int64_t task = qlo + base + __popcll(m & ((1ull << leader) - 1ull));
         if (task >= qhi) {
-          exhausted = true;
+          all_drained = true;
         } else {
           taxon = task % T;
-          const int kind = (int)(task / T);  // kAll: 0 PMD, 1 null; kFR: 0 PMD-f 1 PMD-r 2 null-f 3 null-r
-          pmd = KIND == kAll ? kind == 0 : kind < 2;
-          const bool rev = KIND == kFR && (kind & 1);
-          sub = KIND == kAll ? kind : 2 + kind;
-#pragma unroll
-          for (int i = 0; i < P; ++i) {
-            const PointData pd = slot_point<KIND>(r, i, pmd);
-            const int col = pd.valid ? (KIND == kAll ? r + G * i : pd.k + (rev ? kNHalf : 0)) : 0;
-            s_py[i][lane] = pd.valid ? (double)gy[taxon * kLD + col] : 0.0;
-            s_pN[i][lane] = pd.valid ? (double)gN[taxon * kLD + col] : 0.0;
-          }
-          active = true;
+          sub = (int)(task / T);  // 0 PMD-all, 1 null-all
+          mode = kAllFit;
           starting = true;
         }
       }
     }
-    if (!__any(active)) break;
-
-    // ---- 2. initial point of freshly started sub-fits (oracle: init_u) -----
-    if (__any(starting)) {
-      double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // y,N over all, |z|=1, |z|=2, |z|>=10
-#pragma unroll
-      for (int i = 0; i < P; ++i) {
-        const PointData pd = slot_point<KIND>(r, i, pmd);
-        const double y = s_py[i][lane], N = s_pN[i][lane];  // 0 on pad slots
-        s[0] += y;
-        s[1] += N;
-        if (pd.k == 0) { s[2] += y; s[3] += N; }
-        if (pd.k == 1) { s[4] += y; s[5] += N; }
-        if (pd.k >= 9) { s[6] += y; s[7] += N; }
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s[j] = gsum<G>(s[j]);
-      if (starting) {
-        double u0[4];
-        u0[3] = log(100.0);
-        if (!pmd) {
-          u0[0] = logit(clampd((s[0] + 0.5) / (s[1] + 1.0), 1e-4, 0.9));
-          u0[1] = u0[2] = 0.0;
+    // ---- 2. then fwd/rev pairs, released by finished all-position fits -------
+    const bool need2 = mode == kIdle && all_drained && !ring_drained;
+    if (__any(need2)) {
+      int j = 0;
+      if (need2 && r == 0) j = atomicAdd(ws + kWsPop, 1);
+      j = __shfl(j, leader);
+      if (need2) {
+        if (j >= nall) {
+          ring_drained = true;
         } else {
-          const double c0 = clampd((s[6] + 0.5) / (s[7] + 1.0), 1e-4, 0.3);
-          const double r1 = (s[2] + 0.5) / (s[3] + 1.0);
-          const double r2 = (s[4] + 0.5) / (s[5] + 1.0);
-          const double A0 = clampd(r1 - c0, 1e-3, 0.9 * (1.0 - c0));
-          double q0 = 1.0 / 3.0;
-          if (r1 - c0 > 1e-3) q0 = clampd(1.0 - (r2 - c0) / (r1 - c0), 0.05, 0.95);
-          u0[0] = logit(q0);
-          u0[1] = logit(A0);
-          u0[2] = c0;
+          slot = j;
+          mode = kWaitRing;
         }
-        if (KIND == kFR) {  // warm start at the K1 mode of the same model if it converged
-          const double* base = diag(out, taxon, pmd ? 0 : 1);
-          if (base[6] == (double)MDFIT_OK) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) u0[j] = base[j];
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) u[j] = ut[j] = u0[j];
-        th = make_theta(pmd, ut);
-        curF = INFINITY;
-        curMag = curPg = 0.0;
-        t = 1.0;
-        evals = 0;
-        status = MDFIT_MAXITER;
-        first = true;
       }
     }
+    if (__any(mode == kWaitRing)) {  // poll (acquire: the u0 the producer wrote is visible)
+      int v = 0;
+      if (mode == kWaitRing)
+        v = __hip_atomic_load(ring + slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      if (mode == kWaitRing && v != 0) {
+        const int64_t task = v - 1;
+        taxon = task % T;
+        const bool pmdm = task < T;
+        sub = pmdm ? 2 + h : 4 + h;  // PMD-f/r or null-f/r
+        mode = kPairFit;
+        starting = true;
+      }
+    }
+    if (starting) {
+      pd.pmd = sub == 0 || sub == 2 || sub == 3;
+      pd.y = pd.valid ? (double)gy[taxon * kLD + col] : 0.0;
+      pd.N = pd.valid ? (double)gN[taxon * kLD + col] : 0.0;
+      const double* dg = diag(out, taxon, sub);  // u0: K0 init, or the all-position mode
+#pragma unroll
+      for (int j = 0; j < 4; ++j) u[j] = ut[j] = dg[j];
+      curF = INFINITY;
+      curMag = curPg = 0.0;
+      t = 1.0;
+      evals = 0;
+      status = MDFIT_MAXITER;
+      first = true;
+      running = true;
+    }
+    if (__any(starting)) th = make_theta(pd.pmd, ut);  // unchanged for running fits
+    if (!__any(mode != kIdle || !ring_drained)) break;
 #ifdef MDFIT_STAMP
     const unsigned long long e0 = stamp();
 #endif
+    if (!__any(running)) {  // only waiting groups: back off briefly
+      __builtin_amdgcn_s_sleep(8);
+      continue;
+    }
 
     // ---- 3. value + gradient + Hessian at the trial point --------------------
     double acc[kNAcc];
 #pragma unroll
     for (int j = 0; j < kNAcc; ++j) acc[j] = 0.0;
-#pragma unroll 1
-    for (int i = 0; i < P; ++i) {  // one point at a time: registers
-      PointData pd = slot_point<KIND>(r, i, pmd);
-      pd.y = s_py[i][lane];
-      pd.N = s_pN[i][lane];
-      point_accum(pd, th, acc);
-    }
+    point_accum(pd, th, acc);
 #ifdef MDFIT_STAMP
     const unsigned long long e1 = stamp();
 #endif
+    // sums over the half (16 lanes); all-position fits add the other half
+    const bool whole = mode == kAllFit;
 #pragma unroll
-    for (int j = 0; j < kNAcc; ++j) acc[j] = gsum<G>(acc[j]);
+    for (int j = 0; j < kNAcc; ++j) {
+      const double s16 = gsum<16>(acc[j]);
+      const double s32 = s16 + __shfl_xor(s16, 16, 64);
+      acc[j] = whole ? s32 : s16;
+    }
 #ifdef MDFIT_STAMP
     const unsigned long long e2 = stamp();
 #endif
 
     // ---- 4. Newton logic (oracle: fit_one) ----------------------------------
-    if (active) {
+    if (running) {
       Eval tr;
-      finish_eval(pmd, th, acc, tr);
+      finish_eval(pd.pmd, th, acc, tr);
       ++evals;
       bool accept, done = false;
       if (first) {
@@ -252,7 +295,7 @@ void fit_tasks_kernel(
         curMag = tr.mag;
         curPg = pgnorm(u, tr.g);
         if (!done) {
-          newton_dir(pmd, u, tr.g, tr.H, d);
+          newton_dir(pd.pmd, u, tr.g, tr.H, d);
           t = 1.0;
           if (maxabs4(d) <= tol) {
             done = true;
@@ -273,20 +316,33 @@ void fit_tasks_kernel(
       if (!done) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) ut[j] = clampd(u[j] + t * d[j], kULo[j], kUHi[j]);
-        th = make_theta(pmd, ut);
+        th = make_theta(pd.pmd, ut);
       } else {
-        if (r == 0) {
-          double* dg = diag(out, taxon, sub);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) dg[j] = u[j];
-          dg[4] = curF;
-          dg[5] = (double)evals;
-          dg[6] = (double)status;
-          dg[7] = 0.0;
+        // lanes 0..7 of the half write the diag slots (for an all-position fit
+        // the forward half only); a converged all-position fit also seeds the
+        // u0 of its forward / reverse fits, then releases that pair
+        const int i = r & 15;
+        const bool writer = (!whole || h == 0) && i < 8;
+        if (writer) {
+          const double v = i < 4 ? sel4(u, i)
+                                 : (i == 4 ? curF : (i == 5 ? (double)evals : (i == 6 ? (double)status : 0.0)));
+          diag(out, taxon, sub)[i] = v;
+          if (whole && status == MDFIT_OK && i < 4) {
+            diag(out, taxon, pd.pmd ? 2 : 4)[i] = v;
+            diag(out, taxon, pd.pmd ? 3 : 5)[i] = v;
+          }
         }
-        active = false;
+        if (whole && r == 0) {
+          const int idx = atomicAdd(ws + kWsPush, 1);
+          __hip_atomic_store(ring + idx, (int)(sub * T + taxon) + 1, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+        running = false;
       }
     }
+    // a group is free when neither half is running
+    const unsigned long long busy = __ballot(running);
+    if (((busy >> leader) & 0xFFFFFFFFull) == 0ull && (mode == kAllFit || mode == kPairFit)) mode = kIdle;
 #ifdef MDFIT_STAMP
     const unsigned long long l1 = stamp();
     st_fetch += e0 - f0;
@@ -298,7 +354,7 @@ void fit_tasks_kernel(
   }
 #ifdef MDFIT_STAMP
   if (lane == 0 && g_stamp != nullptr) {
-    unsigned long long* rr = g_stamp + ((int64_t)KIND * 65536 + blockIdx.x) * 8;
+    unsigned long long* rr = g_stamp + (int64_t)blockIdx.x * 8;
     rr[0] = st_eval;
     rr[1] = st_red;
     rr[2] = st_logic;
@@ -628,40 +684,27 @@ template <int KIND>
 __device__ void objective_group(const uint32_t* gy, const uint32_t* gN, int64_t i, bool pmd,
                                 bool rev, const double u[4], double* F, double* g, double* H,
                                 double* ell_out) {
-  constexpr int G = KIND == kAll ? kLanesAll : kLanesAll / 2;
-  constexpr int SLOTS = KIND == kAll ? 32 : 16;
-  constexpr int P = SLOTS / G;
+  constexpr int G = KIND == kAll ? 32 : 16;
+  constexpr int NP = KIND == kAll ? kNPos : kNHalf;
   const int lane = threadIdx.x;
   const int r = lane % G;
-  const bool mine = lane < G;
-  PointData pts[P];
-#pragma unroll
-  for (int k = 0; k < P; ++k) {
-    const int p = r + G * k;
-    PointData& pd = pts[k];
-    pd.pmd = pmd;
-    pd.valid = mine && p < (KIND == kAll ? kNPos : kNHalf);
-    const int col = pd.valid ? (KIND == kAll ? p : p + (rev ? kNHalf : 0)) : 0;
-    pd.k = pd.valid ? (KIND == kAll ? (p < kNHalf ? p : p - kNHalf) : p) : 0;
-    pd.y = pd.valid ? (double)gy[i * kLD + col] : 0.0;
-    pd.N = pd.valid ? (double)gN[i * kLD + col] : 0.0;
-  }
+  PointData pd;
+  pd.pmd = pmd;
+  pd.valid = lane < G && r < NP;
+  pd.k = pd.valid ? (KIND == kAll ? kpos(r) : r) : 0;
+  const int col = pd.valid ? r + (KIND == kFR && rev ? kNHalf : 0) : 0;
+  pd.y = pd.valid ? (double)gy[i * kLD + col] : 0.0;
+  pd.N = pd.valid ? (double)gN[i * kLD + col] : 0.0;
   const Theta th = make_theta(pmd, u);
   double acc[kNAcc];
 #pragma unroll
   for (int j = 0; j < kNAcc; ++j) acc[j] = 0.0;
-  double ell[P];
-#pragma unroll
-  for (int k = 0; k < P; ++k) ell[k] = point_accum(pts[k], th, acc);
+  const double ell = point_accum(pd, th, acc);
 #pragma unroll
   for (int j = 0; j < kNAcc; ++j) acc[j] = gsum<G>(acc[j]);
   Eval e;
   finish_eval(pmd, th, acc, e);
-#pragma unroll
-  for (int k = 0; k < P; ++k) {
-    const int p = r + G * k;
-    if (pts[k].valid) ell_out[i * kNPos + p + (KIND == kFR && rev ? kNHalf : 0)] = ell[k];
-  }
+  if (pd.valid) ell_out[i * kNPos + col] = ell;
   if (lane == 0) {
     F[i] = e.F;
 #pragma unroll
@@ -746,7 +789,11 @@ void mdfit_default_opts(mdfit_opts* o) {
   o->num_samples = 1000;
 }
 
-int64_t mdfit_workspace_bytes(void) { return 256; }
+int64_t mdfit_workspace_bytes(int64_t n_taxa) {
+  if (n_taxa < 0) return 0;
+  const int64_t b = 4 * (mdfit::kWsRing + 2 * n_taxa);
+  return (b + 255) / 256 * 256;
+}
 
 int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t n_taxa,
                     const mdfit_opts* opts, double* out, float* pred, int32_t* status,
@@ -762,17 +809,17 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   if (o.max_iter < 1) return set_err(MDFIT_E_ARG, "max_iter < 1");
   if (n_taxa > ((int64_t)1 << 29)) return set_err(MDFIT_E_ARG, "n_taxa exceeds 2^29 per call");
   hipStream_t s = (hipStream_t)hip_stream;
-  int* queue = (int*)workspace;
-  if (hipMemsetAsync(queue, 0, 2 * mdfit::kQueues * sizeof(int), s) != hipSuccess)
+  int* ws = (int*)workspace;
+  if (hipMemsetAsync(ws, 0, (size_t)mdfit_workspace_bytes(n_taxa), s) != hipSuccess)
     return check_launch("hipMemsetAsync(workspace)");
-  const int64_t gA = fit_grid(mdfit::fit_tasks_kernel<mdfit::kAll>, 2 * n_taxa, mdfit::kWave / mdfit::kLanesAll);
-  hipLaunchKernelGGL(mdfit::fit_tasks_kernel<mdfit::kAll>, dim3((unsigned)gA), dim3(mdfit::kWave), 0, s,
-                     y, N, n_taxa, o.max_iter, o.tol_step, out, queue);
-  if (int rc = check_launch("fit_tasks_kernel<all>")) return rc;
-  const int64_t gB = fit_grid(mdfit::fit_tasks_kernel<mdfit::kFR>, 4 * n_taxa, 2 * mdfit::kWave / mdfit::kLanesAll);
-  hipLaunchKernelGGL(mdfit::fit_tasks_kernel<mdfit::kFR>, dim3((unsigned)gB), dim3(mdfit::kWave), 0, s,
-                     y, N, n_taxa, o.max_iter, o.tol_step, out, queue);
-  if (int rc = check_launch("fit_tasks_kernel<fwd/rev>")) return rc;
+  const int64_t n_init = MDFIT_NSUBFIT * n_taxa;
+  hipLaunchKernelGGL(mdfit::init_kernel, dim3((unsigned)((n_init + 255) / 256)), dim3(256), 0, s, y, N,
+                     n_taxa, out);
+  if (int rc = check_launch("init_kernel")) return rc;
+  const int64_t g = fit_grid(mdfit::fit_kernel, 2 * n_taxa, 2);
+  hipLaunchKernelGGL(mdfit::fit_kernel, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, y, N, n_taxa,
+                     o.max_iter, o.tol_step, out, ws);
+  if (int rc = check_launch("fit_kernel")) return rc;
   hipLaunchKernelGGL(mdfit::assemble_kernel, dim3((unsigned)n_taxa), dim3(mdfit::kWave), 0, s, y, N,
                      mm, n_taxa, out, pred, status);
   return check_launch("assemble_kernel");

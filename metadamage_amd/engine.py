@@ -35,7 +35,7 @@ class FitBatch:
     out: "object"  # torch.float64 [T, NOUT]
     pred: "object"  # torch.float32 [T, 3, 30]
     status: "object"  # torch.int32 [T]
-    workspace: "object" = None  # torch.uint8 [mdfit_workspace_bytes()] (task-queue counters)
+    workspace: "object" = None  # torch.uint8 [mdfit_workspace_bytes(T)] (work queues)
 
 
 def to_device_counts(y, N, mm=None, device="cuda"):
@@ -65,13 +65,13 @@ def alloc_outputs(n_taxa: int, device="cuda", with_pred: bool = True) -> FitBatc
         else None
     )
     status = torch.empty((n_taxa,), dtype=torch.int32, device=device)
-    return FitBatch(out, pred, status, alloc_workspace(device))
+    return FitBatch(out, pred, status, alloc_workspace(n_taxa, device))
 
 
-def alloc_workspace(device="cuda"):
-    """Device scratch mdfit_fit_batch needs (its task-queue counters)."""
+def alloc_workspace(n_taxa: int, device="cuda"):
+    """Device scratch mdfit_fit_batch needs for n_taxa taxa (its work queues)."""
     torch = _torch()
-    return torch.empty((int(_lib.load().mdfit_workspace_bytes()),), dtype=torch.uint8, device=device)
+    return torch.empty((int(_lib.load().mdfit_workspace_bytes(int(n_taxa))),), dtype=torch.uint8, device=device)
 
 
 def fit_batch_device(ty, tN, tm=None, opts: _lib.MdfitOpts | None = None, res: FitBatch | None = None,
@@ -87,8 +87,8 @@ def fit_batch_device(ty, tN, tm=None, opts: _lib.MdfitOpts | None = None, res: F
         raise ValueError("mm must be a contiguous cuda tensor of T*30*12 uint32")
     if res is None:
         res = alloc_outputs(T, device=ty.device)
-    if res.workspace is None:
-        res.workspace = alloc_workspace(ty.device)
+    if res.workspace is None or res.workspace.numel() < lib.mdfit_workspace_bytes(T):
+        res.workspace = alloc_workspace(T, ty.device)
     o = opts if opts is not None else _lib.default_opts()
     _lib.check(
         lib.mdfit_fit_batch(

@@ -39,7 +39,7 @@ def main() -> None:
     b = generate(a.taxa, seed=1)
     ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm)
     res = engine.alloc_outputs(a.taxa)
-    stamps = torch.zeros((2, 65536, 8), dtype=torch.int64, device="cuda")
+    stamps = torch.zeros((65536, 8), dtype=torch.int64, device="cuda")
     lib.mdfit_set_stamp(ctypes.c_void_p(stamps.data_ptr()))
     o = _lib.default_opts()
     for _ in range(2):  # second call is the measured one
@@ -52,9 +52,8 @@ def main() -> None:
         torch.cuda.synchronize()
     s = stamps.cpu().numpy()
     out = res.out.cpu().numpy()
-    for kind, name in ((0, "K1 all"), (1, "K2 fwd/rev")):
-        w = s[kind]
-        w = w[w[:, 4] > 0]
+    for name in ("fit_kernel",):
+        w = s[s[:, 4] > 0]
         tot = w[:, 5].astype(float)
         print(f"{name}: waves {len(w)}  trips/wave {w[:, 4].mean():.1f}  total cyc/wave {tot.mean():.0f} "
               f"(max {tot.max():.0f})")
