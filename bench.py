@@ -39,9 +39,12 @@ sys.path.insert(0, str(ROOT))
 
 TAXA_PER_GPU = 10_000
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-# algorithmic bytes per taxon: y,N 2x30x4 + mismatch 30x12x4 in,
-# 25 result fields x8 + predictions 3x30x4 + status 4 out
-ALG_BYTES_PER_TAXON = 240 + 1440 + 200 + 360 + 4
+# algorithmic bytes per taxon:
+#  whole call: y,N 2x30x4 + mismatch 30x12x4 in, 25 result fields x8 +
+#              predictions 3x30x4 + status 4 out
+#  fit_kernel: y,N 2x30x4 + 6 initial points 6x4x8 in, 6 sub-fit records 6x8x8 out
+CALL_BYTES_PER_TAXON = 240 + 1440 + 200 + 360 + 4
+FIT_BYTES_PER_TAXON = 240 + 192 + 384
 NPTS = np.array([30, 30, 15, 15, 15, 15])
 
 
@@ -57,9 +60,9 @@ def parse():
 
 
 def pmc_traffic():
-    """Per-launch HBM bytes of the fit kernel from the committed rocprofv3 PMC
-    summary (profiles/pmc_fit_map_kernel.json), or None."""
-    f = ROOT / "profiles" / "pmc_fit_map_kernel.json"
+    """Per-launch HBM bytes of fit_kernel from the committed rocprofv3 PMC
+    summary (profiles/pmc_fit_kernel.json), or None."""
+    f = ROOT / "profiles" / "pmc_fit_kernel.json"
     if not f.exists():
         return None
     try:
@@ -100,25 +103,23 @@ def main():
     opts = _lib.default_opts()
     stream = torch.cuda.current_stream(dev)
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
+    def step():
         engine.fit_batch_device(ty, tN, tm, opts, res, stream=stream)
-        if ev is not None:
-            ev[1].record(stream)
         if world > 1:
             gather_records(rec, T, rank, world)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events on the launch stream, recorded by the library around each
+    # call and around fit_kernel (torch events see only torch's stream)
+    engine.profile_enable(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(events[i])
+        step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -127,20 +128,26 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kernel_ms = np.array([a.elapsed_time(b_) for a, b_ in events])
+    call_ms_sum, fit_ms_sum, n_calls = engine.profile_read()
+    engine.profile_enable(False)
+    assert n_calls == min(args.steps, 256), (n_calls, args.steps)  # the library keeps up to 256 calls
 
     # per-rank diagnostics of the last step
     o = out.cpu().numpy()
     st = status.cpu().numpy()
     evals = o[:, _lib.F_DIAG + 5 :: _lib.DIAG_STRIDE][:, :6]
     useful_pe = float((evals * NPTS).sum())
-    lane_pe = float(64 * (np.maximum(evals[:, 0], evals[:, 1]) + evals[:, 2:].max(1)).sum())
+    # position slots the fit kernel's 32-lane groups spent: an all-position fit
+    # holds 30 slots per evaluation, a fwd/rev pair 2x15 until its longer half ends
+    group_evals = evals[:, 0] + evals[:, 1] + np.maximum(evals[:, 2], evals[:, 3]) + np.maximum(evals[:, 4], evals[:, 5])
+    slot_pe = float(30 * group_evals.sum())
 
     if rank == 0:
         total = T * world * args.steps
         value = total / elapsed
-        k_avg_s = float(kernel_ms.mean()) / 1e3
-        achieved = ALG_BYTES_PER_TAXON * T / k_avg_s / 1e9
+        k_avg_s = fit_ms_sum / n_calls / 1e3
+        call_avg_s = call_ms_sum / n_calls / 1e3
+        achieved = FIT_BYTES_PER_TAXON * T / k_avg_s / 1e9
         traffic = pmc_traffic()
         # compute roofline: register-only probe of the same point evaluation
         n_waves, iters = 256 * 16, 64
@@ -151,7 +158,7 @@ def main():
             engine.peak_probe(n_waves, iters, stream=stream)
         e1.record(stream)
         torch.cuda.synchronize(dev)
-        probe_rate = 3 * n_waves * 64 * iters / (e0.elapsed_time(e1) / 1e3)
+        probe_rate = 3 * n_waves * 60 * iters / (e0.elapsed_time(e1) / 1e3)  # 60 points per wave-iteration
         useful_rate = useful_pe / k_avg_s
         line = {
             "metric": "TaxID damage fits/sec",
@@ -180,9 +187,12 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "fit_map_kernel",
-                "kernel_ms_avg": round(float(kernel_ms.mean()), 4),
-                "bytes_per_taxon": ALG_BYTES_PER_TAXON,
+                "kernel": "fit_kernel",
+                "kernel_ms_avg": round(k_avg_s * 1e3, 4),
+                "bytes_per_taxon": FIT_BYTES_PER_TAXON,
+                "call_ms_avg": round(call_avg_s * 1e3, 4),
+                "call_bytes_per_taxon": CALL_BYTES_PER_TAXON,
+                "call_achieved": round(CALL_BYTES_PER_TAXON * T / call_avg_s / 1e9, 3),
             },
             "compute_roofline": {
                 "bound": "fp64-valu",
@@ -190,7 +200,7 @@ def main():
                 "peak": round(probe_rate, 1),
                 "unit": "point-evals/s",
                 "frac": useful_rate / probe_rate,
-                "lane_slot_frac": (lane_pe / k_avg_s) / probe_rate,
+                "slot_util": useful_pe / slot_pe,
                 "point_evals_per_taxon": useful_pe / T,
             },
             "status_ok_frac": float((st == 0).mean()),

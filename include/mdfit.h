@@ -175,6 +175,13 @@ int mdfit_objective(const int32_t* model, const int32_t* subset, const uint32_t*
  */
 int mdfit_peak_probe(int64_t n_waves, int32_t iters, double* sink, void* hip_stream);
 
+/* Profiling hooks (bench / roofline): while enabled, every mdfit_fit_batch
+ * records HIP events on its stream around the whole call and around the fit
+ * kernel (up to 256 calls).  mdfit_profile_read synchronises on them and
+ * returns the summed milliseconds and the number of calls, then resets. */
+int mdfit_profile_enable(int on);
+int mdfit_profile_read(double* call_ms, double* fit_ms, int32_t* n_calls);
+
 const char* mdfit_last_error(void);
 int mdfit_abi_version(void);
 

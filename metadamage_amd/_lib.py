@@ -69,6 +69,8 @@ EXPORTED_SYMBOLS = [
     "mdfit_special",
     "mdfit_peak_probe",
     "mdfit_objective",
+    "mdfit_profile_enable",
+    "mdfit_profile_read",
     "mdfit_last_error",
     "mdfit_abi_version",
 ]
@@ -110,6 +112,11 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.mdfit_fit_batch.argtypes = [vp, vp, vp, i64, ctypes.POINTER(MdfitOpts), vp, vp, vp, vp, vp]
     lib.mdfit_fit_batch.restype = ctypes.c_int
     lib.mdfit_workspace_bytes.argtypes = [i64]
+    if hasattr(lib, "mdfit_profile_enable"):  # (absent from older dev builds loaded by tools/)
+        lib.mdfit_profile_enable.argtypes = [ctypes.c_int]
+        lib.mdfit_profile_enable.restype = ctypes.c_int
+        lib.mdfit_profile_read.argtypes = [vp, vp, vp]
+        lib.mdfit_profile_read.restype = ctypes.c_int
     lib.mdfit_workspace_bytes.restype = i64
     lib.mdfit_betabinom_logpmf.argtypes = [vp, vp, vp, vp, i64, vp, vp, vp]
     lib.mdfit_betabinom_logpmf.restype = ctypes.c_int

@@ -156,7 +156,8 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
   pd.y = pd.N = 0.0;
   pd.pmd = true;
 
-  int mode = kIdle, slot = 0;
+  int mode = kIdle, slot = 0, pollv = 0;
+  bool polled = false, publish = false;
   bool all_drained = false, ring_drained = false;
   // the sub-fit of this lane's half (replicated on its 16 lanes; for an
   // all-position fit both halves hold identical state)
@@ -164,12 +165,12 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
   int sub = 0;
   bool running = false;
   double u[4] = {0, 0, 0, 0}, ut[4] = {0, 0, 0, 0}, d[4] = {0, 0, 0, 0};
-  Theta th = make_theta(true, u);
   double curF = INFINITY, curMag = 0.0, curPg = 0.0, t = 1.0;
   int evals = 0, status = MDFIT_MAXITER;
   bool first = true;
 #ifdef MDFIT_STAMP
   unsigned long long st_eval = 0, st_red = 0, st_logic = 0, st_fetch = 0, st_trips = 0;
+  unsigned long long st_claim1 = 0, st_claim2 = 0;
   const unsigned long long k0 = stamp();
 #endif
 
@@ -180,6 +181,9 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
     bool starting = false;
     // ---- 1. idle groups pull an all-position task (one atomic per wave-trip) --
     const bool need1 = mode == kIdle && !all_drained;
+#ifdef MDFIT_STAMP
+    const unsigned long long a0 = stamp();
+#endif
     if (__any(need1)) {
       const unsigned long long m = __ballot(need1 && r == 0);
       int base = 0;
@@ -190,13 +194,17 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         if (task >= qhi) {
           all_drained = true;
         } else {
-          taxon = task % T;
-          sub = (int)(task / T);  // 0 PMD-all, 1 null-all
+          sub = task < T ? 0 : 1;  // 0 PMD-all, 1 null-all (task < 2T: no division)
+          taxon = task - (sub ? T : 0);
           mode = kAllFit;
           starting = true;
         }
       }
     }
+#ifdef MDFIT_STAMP
+    const unsigned long long a1 = stamp();
+    st_claim1 += a1 - a0;
+#endif
     // ---- 2. then fwd/rev pairs, released by finished all-position fits -------
     const bool need2 = mode == kIdle && all_drained && !ring_drained;
     if (__any(need2)) {
@@ -212,18 +220,20 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         }
       }
     }
-    if (__any(mode == kWaitRing)) {  // poll (acquire: the u0 the producer wrote is visible)
-      int v = 0;
-      if (mode == kWaitRing)
-        v = __hip_atomic_load(ring + slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-      if (mode == kWaitRing && v != 0) {
-        const int64_t task = v - 1;
-        taxon = task % T;
-        const bool pmdm = task < T;
-        sub = pmdm ? 2 + h : 4 + h;  // PMD-f/r or null-f/r
-        mode = kPairFit;
-        starting = true;
-      }
+#ifdef MDFIT_STAMP
+    st_claim2 += stamp() - a1;
+#endif
+    // a waiting group reads the poll it issued last trip (relaxed, its latency
+    // hidden behind that trip's evaluation); the acquire fence then makes the
+    // pair's u0, written before the producer's release, visible
+    const bool ready = mode == kWaitRing && polled && pollv != 0;
+    if (__any(ready)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (ready) {
+      const int64_t task = pollv - 1;
+      taxon = task < T ? task : task - T;
+      sub = task < T ? 2 + h : 4 + h;  // PMD-f/r or null-f/r
+      mode = kPairFit;
+      starting = true;
     }
     if (starting) {
       pd.pmd = sub == 0 || sub == 2 || sub == 3;
@@ -240,21 +250,23 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       first = true;
       running = true;
     }
-    if (__any(starting)) th = make_theta(pd.pmd, ut);  // unchanged for running fits
     if (!__any(mode != kIdle || !ring_drained)) break;
 #ifdef MDFIT_STAMP
     const unsigned long long e0 = stamp();
 #endif
+    polled = mode == kWaitRing;
+    if (polled) pollv = __hip_atomic_load(ring + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!__any(running)) {  // only waiting groups: back off briefly
       __builtin_amdgcn_s_sleep(8);
       continue;
     }
 
     // ---- 3. value + gradient + Hessian at the trial point --------------------
+    const Theta th = make_theta(pd.pmd, ut);  // row-collective: every lane
     double acc[kNAcc];
 #pragma unroll
     for (int j = 0; j < kNAcc; ++j) acc[j] = 0.0;
-    point_accum(pd, th, acc);
+    point_accum<true>(pd, th, acc);
 #ifdef MDFIT_STAMP
     const unsigned long long e1 = stamp();
 #endif
@@ -316,7 +328,6 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       if (!done) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) ut[j] = clampd(u[j] + t * d[j], kULo[j], kUHi[j]);
-        th = make_theta(pd.pmd, ut);
       } else {
         // lanes 0..7 of the half write the diag slots (for an all-position fit
         // the forward half only); a converged all-position fit also seeds the
@@ -332,13 +343,24 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
             diag(out, taxon, pd.pmd ? 3 : 5)[i] = v;
           }
         }
-        if (whole && r == 0) {
-          const int idx = atomicAdd(ws + kWsPush, 1);
-          __hip_atomic_store(ring + idx, (int)(sub * T + taxon) + 1, __ATOMIC_RELEASE,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        }
+        publish = whole && r == 0;
         running = false;
       }
+    }
+    // release the finished all-position fits' fwd/rev pairs (MI355X_MICROARCH
+    // hand-off recipe: stores -> wait -> agent release -> wait -> ticket ->
+    // relaxed flag; the explicit waits keep ROCm 7.2 from dropping the
+    // fence's own wait, which would let the flag overtake the write-back)
+    if (__any(publish)) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (publish) {
+        const int idx = atomicAdd(ws + kWsPush, 1);
+        __hip_atomic_store(ring + idx, (int)(sub * T + taxon) + 1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+      publish = false;
     }
     // a group is free when neither half is running
     const unsigned long long busy = __ballot(running);
@@ -361,6 +383,8 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
     rr[3] = st_fetch;
     rr[4] = st_trips;
     rr[5] = stamp() - k0;
+    rr[6] = st_claim1;
+    rr[7] = st_claim2;
   }
 #endif
 }
@@ -650,25 +674,28 @@ __global__ void betabinom_kernel(const double* __restrict__ y, const double* __r
   }
 }
 
-// Register-only throughput probe: each lane evaluates point_accum `iters`
-// times on a representative argument mix (a needs the small-x shift, the
-// others do not -- as in typical fits).
+// Register-only throughput probe of the fit kernel's point evaluation
+// (make_theta + point_accum<kRowPhi>, the row layout of fit_kernel: lane 15 of
+// every row a pad): each wave evaluates `iters` times 60 points on a
+// representative argument mix (a needs the small-x shift, the others do not --
+// as in typical fits).  Useful work: 60 point-evaluations per wave-iteration.
 __global__ __launch_bounds__(kWave) void peak_probe_kernel(int iters, double* __restrict__ sink) {
   const int lane = threadIdx.x;
+  const int i = lane & 15;
   PointData pd;
-  pd.valid = true;
+  pd.valid = i < kNHalf;
   pd.pmd = true;
-  pd.k = lane % kNHalf;
-  pd.N = 1.0e5 + 1000.0 * lane;
+  pd.k = pd.valid ? i : 0;
+  pd.N = pd.valid ? 1.0e5 + 1000.0 * lane : 0.0;
   pd.y = 0.01 * pd.N;
-  const double u[4] = {-0.5, -3.0, 0.01, 6.0};
-  Theta th = make_theta(true, u);
+  double u[4] = {-0.5, -3.0, 0.01, 6.0};
   double acc[kNAcc];
 #pragma unroll
   for (int j = 0; j < kNAcc; ++j) acc[j] = 0.0;
   for (int it = 0; it < iters; ++it) {
-    point_accum(pd, th, acc);
-    th.phi += 1e-12 * acc[0];  // loop-carried dependence: no hoisting
+    const Theta th = make_theta(true, u);
+    point_accum<true>(pd, th, acc);
+    u[3] += 1e-12 * rowb<0>(acc[0]);  // loop-carried, row-uniform: no hoisting
   }
   double s = 0.0;
 #pragma unroll
@@ -677,31 +704,32 @@ __global__ __launch_bounds__(kWave) void peak_probe_kernel(int iters, double* __
 }
 
 // Objective / gradient / Hessian of one sub-fit at a given u, evaluated with
-// the fit kernels' own group layout and code (the group of G lanes at lanes
-// 0..G-1, each lane owning P position slots) -- the parity test of the
-// objective itself.  One wave per item.
+// the fit kernel's own layout and code (all-position: lanes 0..31, halves
+// summed; forward / reverse: lanes 0..15) -- the parity test of the objective
+// itself.  One wave per item; every lane runs (the row-collective pieces).
 template <int KIND>
 __device__ void objective_group(const uint32_t* gy, const uint32_t* gN, int64_t i, bool pmd,
                                 bool rev, const double u[4], double* F, double* g, double* H,
                                 double* ell_out) {
-  constexpr int G = KIND == kAll ? 32 : 16;
-  constexpr int NP = KIND == kAll ? kNPos : kNHalf;
   const int lane = threadIdx.x;
-  const int r = lane % G;
+  const int r = lane & 31, h = r >> 4, k = r & 15;
   PointData pd;
   pd.pmd = pmd;
-  pd.valid = lane < G && r < NP;
-  pd.k = pd.valid ? (KIND == kAll ? kpos(r) : r) : 0;
-  const int col = pd.valid ? r + (KIND == kFR && rev ? kNHalf : 0) : 0;
+  pd.valid = (KIND == kAll ? lane < 32 : lane < 16) && k < kNHalf;
+  pd.k = pd.valid ? k : 0;
+  const int col = pd.valid ? (KIND == kAll ? h : (rev ? 1 : 0)) * kNHalf + k : 0;
   pd.y = pd.valid ? (double)gy[i * kLD + col] : 0.0;
   pd.N = pd.valid ? (double)gN[i * kLD + col] : 0.0;
   const Theta th = make_theta(pmd, u);
   double acc[kNAcc];
 #pragma unroll
   for (int j = 0; j < kNAcc; ++j) acc[j] = 0.0;
-  const double ell = point_accum(pd, th, acc);
+  const double ell = point_accum<true>(pd, th, acc);
 #pragma unroll
-  for (int j = 0; j < kNAcc; ++j) acc[j] = gsum<G>(acc[j]);
+  for (int j = 0; j < kNAcc; ++j) {
+    const double s16 = gsum<16>(acc[j]);
+    acc[j] = KIND == kAll ? s16 + __shfl_xor(s16, 16, 64) : s16;
+  }
   Eval e;
   finish_eval(pmd, th, acc, e);
   if (pd.valid) ell_out[i * kNPos + col] = ell;
@@ -711,7 +739,7 @@ __device__ void objective_group(const uint32_t* gy, const uint32_t* gN, int64_t 
     for (int j = 0; j < 4; ++j) {
       g[i * 4 + j] = e.g[j];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) H[i * 16 + 4 * j + k] = e.H[j <= k ? hidx(j, k) : hidx(k, j)];
+      for (int m = 0; m < 4; ++m) H[i * 16 + 4 * j + m] = e.H[j <= m ? hidx(j, m) : hidx(m, j)];
     }
   }
 }
@@ -774,9 +802,55 @@ int64_t fit_grid(K kernel, int64_t ntask, int fits_per_wave) {
   g = ((g + mdfit::kQueues - 1) / mdfit::kQueues) * mdfit::kQueues;
   return g < mdfit::kQueues ? mdfit::kQueues : g;
 }
+// optional HIP-event timing of mdfit_fit_batch (mdfit_profile_enable):
+// per call, events around the whole call and around fit_kernel, on the
+// caller's stream
+constexpr int kProfMax = 256;
+struct ProfState {
+  bool on = false;
+  int n = 0;
+  hipEvent_t ev[kProfMax][4];
+  bool made = false;
+};
+ProfState g_prof;
+
+void prof_record(int slot, hipStream_t s) {
+  if (g_prof.on && g_prof.n < kProfMax) (void)hipEventRecord(g_prof.ev[g_prof.n][slot], s);
+}
 }  // namespace
 
 extern "C" {
+
+int mdfit_profile_enable(int on) {
+  if (on && !g_prof.made) {
+    for (int i = 0; i < kProfMax; ++i)
+      for (int j = 0; j < 4; ++j)
+        if (hipEventCreate(&g_prof.ev[i][j]) != hipSuccess) return set_err(MDFIT_E_HIP, "hipEventCreate");
+    g_prof.made = true;
+  }
+  g_prof.on = on != 0;
+  g_prof.n = 0;
+  return 0;
+}
+
+int mdfit_profile_read(double* call_ms, double* fit_ms, int32_t* n_calls) {
+  if (!call_ms || !fit_ms || !n_calls) return set_err(MDFIT_E_ARG, "null argument");
+  double a = 0.0, b = 0.0;
+  for (int i = 0; i < g_prof.n; ++i) {
+    float x = 0.f, y = 0.f;
+    if (hipEventSynchronize(g_prof.ev[i][3]) != hipSuccess ||
+        hipEventElapsedTime(&x, g_prof.ev[i][0], g_prof.ev[i][3]) != hipSuccess ||
+        hipEventElapsedTime(&y, g_prof.ev[i][1], g_prof.ev[i][2]) != hipSuccess)
+      return set_err(MDFIT_E_HIP, "hipEventElapsedTime");
+    a += x;
+    b += y;
+  }
+  *call_ms = a;
+  *fit_ms = b;
+  *n_calls = g_prof.n;
+  g_prof.n = 0;
+  return 0;
+}
 
 void mdfit_default_opts(mdfit_opts* o) {
   if (!o) return;
@@ -810,6 +884,7 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   if (n_taxa > ((int64_t)1 << 29)) return set_err(MDFIT_E_ARG, "n_taxa exceeds 2^29 per call");
   hipStream_t s = (hipStream_t)hip_stream;
   int* ws = (int*)workspace;
+  prof_record(0, s);
   if (hipMemsetAsync(ws, 0, (size_t)mdfit_workspace_bytes(n_taxa), s) != hipSuccess)
     return check_launch("hipMemsetAsync(workspace)");
   const int64_t n_init = MDFIT_NSUBFIT * n_taxa;
@@ -817,12 +892,17 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
                      n_taxa, out);
   if (int rc = check_launch("init_kernel")) return rc;
   const int64_t g = fit_grid(mdfit::fit_kernel, 2 * n_taxa, 2);
+  prof_record(1, s);
   hipLaunchKernelGGL(mdfit::fit_kernel, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, y, N, n_taxa,
                      o.max_iter, o.tol_step, out, ws);
   if (int rc = check_launch("fit_kernel")) return rc;
+  prof_record(2, s);
   hipLaunchKernelGGL(mdfit::assemble_kernel, dim3((unsigned)n_taxa), dim3(mdfit::kWave), 0, s, y, N,
                      mm, n_taxa, out, pred, status);
-  return check_launch("assemble_kernel");
+  if (int rc = check_launch("assemble_kernel")) return rc;
+  prof_record(3, s);
+  if (g_prof.on && g_prof.n < kProfMax) ++g_prof.n;
+  return 0;
 }
 
 int mdfit_betabinom_logpmf(const double* y, const double* N, const double* alpha,

@@ -76,32 +76,54 @@ __device__ __forceinline__ void logit_parts(double u, double& p, double& omp, do
   l1mp = pos ? -(u + sp) : -sp;
 }
 
-// Constrained parameters of one trial point u (group-uniform), computed once
-// per trial instead of once per point evaluation; kept lean (registers).
+// Broadcast lane N of every 16-lane DPP row to the whole row (row_newbcast).
+template <int N>
+__device__ __forceinline__ double rowb(double v) {
+  return dpp<0x150 + N>(v);
+}
+
+// Constrained parameters of one trial point u, computed once per trial
+// instead of once per point evaluation; kept lean (registers).
 struct Theta {
-  double q, omq, iomq;        // q, 1-q, 1/(1-q)
-  double A, JA;               // A and A(1-A) (PMD only)
-  double c, iomc;             // c and 1/(1-c) (PMD only; c on its own scale)
+  double q, omq, iomq;  // q, 1-q, 1/(1-q)
+  double A, JA;         // A and A(1-A) (PMD only)
+  double c, iomc;       // c and 1/(1-c) (PMD only; c on its own scale)
   double delta, phi;
-  double lprior;              // log prior at u (constants dropped)
+  double lprior;        // log prior at u (constants dropped)
 };
 
+// Row-collective: every lane of a 16-lane row must be active and hold the
+// same u and model (a row never spans two sub-fits).  The transcendental
+// pieces are spread over the row -- lane 0: sigmoid / log-sigmoids of u0,
+// lane 1: of u1, lane 2: exp(u3) and ln(1-c) -- one exp, one log1p and one
+// reciprocal per lane instead of three of each, then broadcast.
 __device__ __forceinline__ Theta make_theta(bool pmd, const double u[4]) {
+  const int i = (int)(threadIdx.x & 15);
+  const double v = i == 0 ? u[0] : u[1];  // the logit this lane resolves (lanes 0, 1)
+  const double e = exp(i < 2 ? -fabs(v) : u[3]);
+  const double sp = flog1p(i < 2 ? e : -u[2]);  // ln(1 + e^-|v|), or ln(1-c) on lane 2
+  const double rr = rcp(1.0 + e);
+  const bool pos = v >= 0.0;
+  const double p = pos ? rr : e * rr, omp = pos ? e * rr : rr;
+  // ln p + 2 ln(1-p)  (fits.py:46-48: Beta(2, 3) prior up to a constant)
+  const double lpp = (pos ? -sp : v - sp) + 2.0 * (pos ? -(v + sp) : -sp);
   Theta th;
-  double lq, l1mq;
-  logit_parts(u[0], th.q, th.omq, lq, l1mq);
+  th.q = rowb<0>(p);
+  th.omq = rowb<0>(omp);
+  const double lpq = rowb<0>(lpp);
+  const double A = rowb<1>(p), omA = rowb<1>(omp), lpA = rowb<1>(lpp);
+  th.delta = rowb<2>(e);
+  const double l1mc = rowb<2>(sp);
   th.iomq = rcp(th.omq);
-  th.delta = exp(u[3]);
   th.phi = th.delta + 2.0;
   // ln q + 2 ln(1-q) - delta/1000  [+ ln A + 2 ln(1-A) + 8 ln(1-c)]  (fits.py:46-53)
-  th.lprior = lq + 2.0 * l1mq - th.delta / 1000.0;
+  th.lprior = lpq - th.delta / 1000.0;
   if (pmd) {
-    double omA, lA, l1mA;
-    logit_parts(u[1], th.A, omA, lA, l1mA);
-    th.JA = th.A * omA;
+    th.A = A;
+    th.JA = A * omA;
     th.c = u[2];
     th.iomc = rcp(1.0 - th.c);
-    th.lprior += lA + 2.0 * l1mA + 8.0 * flog1p(-th.c);
+    th.lprior += lpA + 8.0 * l1mc;
   } else {
     th.A = th.JA = th.c = 0.0;
     th.iomc = 1.0;
@@ -134,6 +156,12 @@ struct PointData {
 // One point's contribution at theta, ADDED to acc (same formulas as
 // oracle/mdfit_oracle.c evaluate(); derivation in DESIGN.md §3).  Returns the
 // point's log-likelihood (without log C(N,y)).
+//
+// kRowPhi: the (lnGamma, psi, psi1) triple at phi is taken from lane 15 of
+// the 16-lane row -- a pad lane (N = 0) whose lg3(N + phi) IS lg3(phi),
+// bitwise -- so a point costs 5 lg3 instead of 6 (row-collective then: all
+// lanes active, lane 15 of every row a pad holding the row's phi).
+template <bool kRowPhi = false>
 __device__ __forceinline__ double point_accum(const PointData& pd, const Theta& th,
                                               double acc[kNAcc]) {
   double D, Dq, DA, Dc, Dqq, DqA;
@@ -166,7 +194,14 @@ __device__ __forceinline__ double point_accum(const PointData& pd, const Theta& 
   const double lb = t2.l - t5.l, Pb = t2.p - t5.p, Qb = t2.q - t5.q;
   mag += fabs(t2.l) + fabs(t5.l);
   const LG3 t3 = lg3(pd.N + phi);
-  const LG3 t6 = lg3(phi);
+  LG3 t6;
+  if (kRowPhi) {
+    t6.l = rowb<15>(t3.l);
+    t6.p = rowb<15>(t3.p);
+    t6.q = rowb<15>(t3.q);
+  } else {
+    t6 = lg3(phi);
+  }
   const double lS = t3.l - t6.l, S = t6.p - t3.p, S1 = t6.q - t3.q;
   mag += fabs(t3.l) + fabs(t6.l);
   const double ell = (la + lb) - lS;  // exact 0 when N = 0

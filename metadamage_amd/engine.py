@@ -152,6 +152,20 @@ def peak_probe(n_waves: int, iters: int, stream=None):
     return sink
 
 
+def profile_enable(on: bool = True) -> None:
+    """Record HIP events around every following mdfit_fit_batch call (and its
+    fit kernel) on the call's stream."""
+    _lib.check(_lib.load().mdfit_profile_enable(1 if on else 0))
+
+
+def profile_read():
+    """(call_ms_sum, fit_kernel_ms_sum, n_calls) over the calls recorded since
+    profile_enable / the last read (synchronises on the events)."""
+    a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int32()
+    _lib.check(_lib.load().mdfit_profile_read(ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)))
+    return a.value, b.value, n.value
+
+
 def objective(model, subset, y, N, u, device="cuda"):
     """Per-item sub-fit objective (F, g[4], H[4,4], ell[30]) evaluated by the
     fit kernel's code path (mdfit_objective)."""

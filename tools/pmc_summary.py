@@ -1,0 +1,73 @@
+"""Summarise the rocprofv3 passes of tools/profile_round.sh into profiles/.
+
+Copies the kernel-trace stats / PMC CSVs of the named round into profiles/ and
+writes profiles/pmc_fit_kernel.json (per-launch HBM bytes of fit_kernel,
+corrected as MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE x2 on gfx950,
+WRITE_SIZE as read; both counters are kB).
+
+    python tools/pmc_summary.py r01 gpurun_out/prof
+"""
+
+from __future__ import annotations
+
+import csv
+import json
+import shutil
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+TAXA = 10_000
+FIT_BYTES_PER_TAXON = 240 + 192 + 384  # bench.py
+
+
+def rows(path: Path):
+    with open(path) as f:
+        yield from csv.DictReader(f)
+
+
+def counter_mean(path: Path, kernel: str, name: str) -> float:
+    v = [float(r["Counter_Value"]) for r in rows(path) if r["Counter_Name"] == name and kernel in r["Kernel_Name"]]
+    if not v:
+        raise SystemExit(f"no {name} rows for {kernel} in {path}")
+    return sum(v) / len(v)
+
+
+def main() -> None:
+    tag, src = sys.argv[1], Path(sys.argv[2])
+    prof = ROOT / "profiles"
+    prof.mkdir(exist_ok=True)
+    found = {}
+    for sub, name, dst in (("trace", "kernel_stats.csv", "kernel_stats.csv"),
+                           ("trace", "kernel_trace.csv", "kernel_trace.csv"),
+                           ("fetch", "counter_collection.csv", "pmc_fetch_size.csv"),
+                           ("write", "counter_collection.csv", "pmc_write_size.csv")):
+        cands = sorted((src / sub).rglob(f"*{name}"))
+        if not cands:
+            raise SystemExit(f"missing {sub}/*{name} under {src}")
+        shutil.copy(cands[0], prof / f"{tag}_{dst}")
+        found[dst] = prof / f"{tag}_{dst}"
+    k = "mdfit::fit_kernel"
+    fetch_kb = counter_mean(found["pmc_fetch_size.csv"], k, "FETCH_SIZE")
+    write_kb = counter_mean(found["pmc_write_size.csv"], k, "WRITE_SIZE")
+    stats = {r["Name"].split("(")[0]: r for r in rows(found["kernel_stats.csv"])}
+    fk = stats.get(k, {})
+    summary = {
+        "kernel": k,
+        "taxa_per_launch": TAXA,
+        "FETCH_SIZE_kB_mean": fetch_kb,
+        "WRITE_SIZE_kB_mean": write_kb,
+        "correction": "gfx950: FETCH_SIZE x2 (MI355X_MICROARCH.md §HBM: FETCH_SIZE reports 1/2 of wide coalesced "
+        "reads; this kernel's 4-B/lane and broadcast 8-B loads are uncalibrated), WRITE_SIZE x1",
+        "hbm_bytes_per_launch": int(round((2 * fetch_kb + write_kb) * 1024)),
+        "algorithmic_bytes_per_launch": FIT_BYTES_PER_TAXON * TAXA,
+        "rocprof_avg_ns": float(fk.get("AverageNs", "nan")),
+        "source": f"rocprofv3 --kernel-trace --stats; --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes; "
+        f"python bench.py (profiles/{tag}_*.csv)",
+    }
+    (prof / "pmc_fit_kernel.json").write_text(json.dumps(summary, indent=1) + "\n")
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()

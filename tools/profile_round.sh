@@ -1,0 +1,17 @@
+#!/bin/bash
+# rocprofv3 passes behind profiles/ (run on the GPU box from the repo root):
+#   bash tools/profile_round.sh r01
+# kernel trace + stats, then FETCH_SIZE and WRITE_SIZE in separate --pmc passes
+# (never combined with trace domains), then the summary.
+set -o pipefail
+TAG=${1:-r01}
+OUT=gpurun_out/prof
+rm -rf "$OUT" && mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
+    python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > "$OUT/bench_trace.json" 2> "$OUT/trace.err" && \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- \
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > /dev/null 2> "$OUT/fetch.err" && \
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- \
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > /dev/null 2> "$OUT/write.err" && \
+python3 tools/pmc_summary.py "$TAG" "$OUT"
