@@ -1,6 +1,7 @@
 #!/bin/bash
 # rocprofv3 passes behind profiles/ (run on the GPU box from the repo root):
-#   bash tools/profile_round.sh r01
+#   bash tools/profile_round.sh r01      (on the box; then locally:
+#   python tools/pmc_summary.py r01 gpurun_out/prof   -> profiles/)
 # kernel trace + stats, then FETCH_SIZE and WRITE_SIZE in separate --pmc passes
 # (never combined with trace domains), then the summary.
 set -o pipefail
