@@ -53,6 +53,7 @@ extern "C" {
 
 /* Fit modes. */
 #define MDFIT_MODE_MAP 0  /* maximum a posteriori of model_PMD / model_null (fits.py:43-67) */
+#define MDFIT_MODE_NUTS 1 /* NUTS posterior sampling as fits.py:382-387 (MDFIT-NUTS v1) */
 
 /* Per-taxon status codes (status[t]). */
 #define MDFIT_OK 0
@@ -109,12 +110,14 @@ enum mdfit_field {
 #define MDFIT_NPRED 3
 
 typedef struct mdfit_opts {
-  int32_t mode;       /* MDFIT_MODE_MAP */
-  int32_t max_iter;   /* objective evaluations per sub-fit (default 200) */
-  double tol_step;    /* convergence: max |Newton step| in unconstrained units (default 1e-9) */
-  uint64_t seed;      /* reserved for the sampling mode */
-  int32_t num_warmup; /* reserved for the sampling mode */
-  int32_t num_samples;/* reserved for the sampling mode */
+  int32_t mode;       /* MDFIT_MODE_MAP or MDFIT_MODE_NUTS */
+  int32_t max_iter;   /* MAP: objective evaluations per sub-fit (default 200) */
+  double tol_step;    /* MAP: convergence, max |Newton step| in unconstrained units (default 1e-9) */
+  uint64_t seed;      /* NUTS: key of the Philox streams (default 0, the reference's Key(0)) */
+  int32_t num_warmup; /* NUTS: adaptation iterations (default 500, fits.py:792-799) */
+  int32_t num_samples;/* NUTS: kept iterations (default 1000) */
+  int64_t index_base; /* NUTS: global index of taxon 0 of this call -- the random streams are keyed
+                         by it, so a sharded run draws the same numbers as one call (default 0) */
 } mdfit_opts;
 
 /* Fill `opts` with defaults. */
@@ -136,8 +139,10 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm,
                     float* pred, int32_t* status, void* workspace,
                     void* hip_stream);
 
-/* Bytes of device workspace mdfit_fit_batch needs for n_taxa taxa. */
-int64_t mdfit_workspace_bytes(int64_t n_taxa);
+/* Bytes of device workspace mdfit_fit_batch needs for n_taxa taxa under
+ * `opts` (NULL = defaults; NUTS keeps every chain's samples there:
+ * 6 x num_samples x 4 doubles per taxon). */
+int64_t mdfit_workspace_bytes(int64_t n_taxa, const mdfit_opts* opts);
 
 /*
  * Pointwise beta-binomial log-pmf (numpyro BetaBinomial.log_prob, used by
@@ -174,6 +179,18 @@ int mdfit_objective(const int32_t* model, const int32_t* subset, const uint32_t*
  * double[n_waves*64].  Used by bench.py for the compute roofline.
  */
 int mdfit_peak_probe(int64_t n_waves, int32_t iters, double* sink, void* hip_stream);
+
+/*
+ * Sampling-mode potential -(log density + log|J|) and its gradient in the
+ * unconstrained v = (logit q, logit A, logit c, log delta) (numpyro's
+ * potential of model_PMD / model_null, fits.py:43-67), evaluated by the chain
+ * kernel's own lane layout and code (parity tests).  Per item i: model[i]
+ * (0 PMD, 1 null), subset[i] (0 all, 1 forward, 2 reverse), y/N rows
+ * [n][MDFIT_LD], v[n][4] -> U[n], g[n][4]; infeasible -> U = +inf, g = 0.
+ */
+int mdfit_nuts_potential(const int32_t* model, const int32_t* subset, const uint32_t* y,
+                         const uint32_t* N, const double* v, int64_t n, double* U, double* g,
+                         void* hip_stream);
 
 /* Profiling hooks (bench / roofline): while enabled, every mdfit_fit_batch
  * records HIP events on its stream around the whole call and around the fit

@@ -21,7 +21,7 @@ NHALF = 15
 LD = 32
 NMM = 12
 NPRED = 3
-MODE_MAP = 0
+MODE_MAP = 0  # (MODE_NUTS below)
 OK, MAXITER, NONFINITE, INVALID = 0, 1, 2, 3
 NRESULT = 25
 F_DIAG = 32
@@ -69,6 +69,7 @@ EXPORTED_SYMBOLS = [
     "mdfit_special",
     "mdfit_peak_probe",
     "mdfit_objective",
+    "mdfit_nuts_potential",
     "mdfit_profile_enable",
     "mdfit_profile_read",
     "mdfit_last_error",
@@ -84,7 +85,12 @@ class MdfitOpts(ctypes.Structure):
         ("seed", ctypes.c_uint64),
         ("num_warmup", ctypes.c_int32),
         ("num_samples", ctypes.c_int32),
+        ("index_base", ctypes.c_int64),
     ]
+
+
+MODE_MAP, MODE_NUTS = 0, 1
+SAMPLES_OFFSET = 256  # NUTS workspace: double[T][6][S][4] draws after the queue counters
 
 
 class MdfitError(RuntimeError):
@@ -111,7 +117,10 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.mdfit_default_opts.restype = None
     lib.mdfit_fit_batch.argtypes = [vp, vp, vp, i64, ctypes.POINTER(MdfitOpts), vp, vp, vp, vp, vp]
     lib.mdfit_fit_batch.restype = ctypes.c_int
-    lib.mdfit_workspace_bytes.argtypes = [i64]
+    lib.mdfit_workspace_bytes.argtypes = [i64, ctypes.c_void_p]
+    if hasattr(lib, "mdfit_nuts_potential"):
+        lib.mdfit_nuts_potential.argtypes = [vp, vp, vp, vp, vp, i64, vp, vp, vp]
+        lib.mdfit_nuts_potential.restype = ctypes.c_int
     if hasattr(lib, "mdfit_profile_enable"):  # (absent from older dev builds loaded by tools/)
         lib.mdfit_profile_enable.argtypes = [ctypes.c_int]
         lib.mdfit_profile_enable.restype = ctypes.c_int

@@ -37,13 +37,12 @@
 #include <cstring>
 
 #include "../../include/mdfit.h"
+#include "mdfit_host.h"
 #include "mdfit_model.h"
 #include "mdfit_special.h"
 
 namespace mdfit {
 
-constexpr int kWave = 64;
-constexpr int kQueues = 8;      // one work queue per XCD (blockIdx % 8 share an XCD)
 constexpr int kAll = 0, kFR = 1;
 
 // diag slots of the out record (include/mdfit.h): during K1/K2 slots 0..3 of a
@@ -566,79 +565,7 @@ __global__ __launch_bounds__(kWave) void assemble_kernel(
     if (lane == 0) s_rec[MDFIT_F_ASYMMETRY] = (wFR - wC) / sqrt(kNPos * var);
   }
 
-  // ---- sums (fits.py:272-283) -------------------------------------------------
-  {
-    const double v = lane < kNPos ? 1.0 : 0.0;
-    const double fw = lane < kNHalf ? 1.0 : 0.0;
-    const int pi = lane < kNPos ? lane : 0;
-    const double yv = v * s_y[pi], nv = v * s_N[pi];
-    const double nf = gsum<64>(fw * nv), nt = gsum<64>(nv);
-    const double yf = gsum<64>(fw * yv), yt = gsum<64>(yv);
-    if (lane == 0) {
-      s_rec[MDFIT_F_N_Z1_FORWARD] = s_N[0];
-      s_rec[MDFIT_F_N_Z1_REVERSE] = s_N[kNHalf];
-      s_rec[MDFIT_F_N_SUM_FORWARD] = nf;
-      s_rec[MDFIT_F_N_SUM_REVERSE] = nt - nf;
-      s_rec[MDFIT_F_N_SUM_TOTAL] = nt;
-      s_rec[MDFIT_F_Y_SUM_FORWARD] = yf;
-      s_rec[MDFIT_F_Y_SUM_REVERSE] = yt - yf;
-      s_rec[MDFIT_F_Y_SUM_TOTAL] = yt;
-    }
-  }
-
-  // ---- noise (fits.py:359-376) -------------------------------------------------
-  {
-    // lane j < 12 owns mismatch column j (AC AG AT CA CG CT GA GC GT TA TC TG);
-    // CT is NaN on rows 0..14, GA on rows 15..29.
-    const int j = lane < kNMM ? lane : 0;
-    const bool own = lane < kNMM && gmm != nullptr;
-    double s = 0.0, cnt = 0.0;
-    for (int i = 0; i < kNPos; ++i) {
-      const bool nanned = (j == 5 && i < kNHalf) || (j == 6 && i >= kNHalf);
-      if (!nanned) {
-        s += (double)s_mm[i * kNMM + j];
-        cnt += 1.0;
-      }
-    }
-    const double m = s / cnt;
-    double sa[3] = {0, 0, 0}, ca[3] = {0, 0, 0};
-    for (int i = 0; i < kNPos; ++i) {
-      const bool nanned = (j == 5 && i < kNHalf) || (j == 6 && i >= kNHalf);
-      const double x = (double)s_mm[i * kNMM + j] / m;
-      if (own && !nanned && !isnan(x)) {
-        const int h = i < kNHalf ? 1 : 2;
-        sa[0] += x;
-        ca[0] += 1.0;
-        sa[h] += x;
-        ca[h] += 1.0;
-      }
-    }
-    double mean[3];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) mean[q] = gsum<16>(sa[q]) / gsum<16>(ca[q]);
-    double ss[3] = {0, 0, 0};
-    for (int i = 0; i < kNPos; ++i) {
-      const bool nanned = (j == 5 && i < kNHalf) || (j == 6 && i >= kNHalf);
-      const double x = (double)s_mm[i * kNMM + j] / m;
-      if (own && !nanned && !isnan(x)) {
-        const int h = i < kNHalf ? 1 : 2;
-        ss[0] += (x - mean[0]) * (x - mean[0]);
-        ss[h] += (x - mean[h]) * (x - mean[h]);
-      }
-    }
-    double nz[3];
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const double c = gsum<16>(ca[q]);
-      nz[q] = c > 0.0 ? sqrt(gsum<16>(ss[q]) / c) : NAN;
-    }
-    if (lane == 0) {
-      const bool have = gmm != nullptr;
-      s_rec[MDFIT_F_NORMALIZED_NOISE] = have ? nz[0] : NAN;
-      s_rec[MDFIT_F_NORMALIZED_NOISE_FORWARD] = have ? nz[1] : NAN;
-      s_rec[MDFIT_F_NORMALIZED_NOISE_REVERSE] = have ? nz[2] : NAN;
-    }
-  }
+  record_sums_noise(lane, s_y, s_N, s_mm, gmm != nullptr, s_rec);
 
   __syncthreads();
   for (int i = lane; i < MDFIT_NOUT; i += kWave) out[t * MDFIT_NOUT + i] = s_rec[i];
@@ -766,7 +693,7 @@ __global__ __launch_bounds__(kWave) void objective_kernel(
 // ===========================================================================
 // C-ABI
 // ===========================================================================
-namespace {
+namespace mdfit::host {
 thread_local char g_err[512] = "";
 
 int set_err(int code, const char* msg) {
@@ -783,25 +710,14 @@ int check_launch(const char* what) {
   g_err[0] = '\0';
   return 0;
 }
+}  // namespace mdfit::host
 
-// persistent grid: no more waves than can be resident at once (so every
-// wave starts immediately and pulls work until its queue is drained), a
-// multiple of the 8 queues
-template <typename K>
-int64_t fit_grid(K kernel, int64_t ntask, int fits_per_wave) {
-  int dev = 0, n_cu = 256, per_cu = 8;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
-    n_cu = 256;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, mdfit::kWave, 0) != hipSuccess ||
-      per_cu <= 0)
-    per_cu = 8;
-  const int64_t want = (ntask + fits_per_wave - 1) / fits_per_wave;
-  const int64_t cap = (int64_t)n_cu * per_cu;
-  int64_t g = want < cap ? want : cap;
-  g = ((g + mdfit::kQueues - 1) / mdfit::kQueues) * mdfit::kQueues;
-  return g < mdfit::kQueues ? mdfit::kQueues : g;
-}
+namespace {
+using mdfit::host::check_launch;
+using mdfit::host::fit_grid;
+using mdfit::host::g_err;
+using mdfit::host::set_err;
+
 // optional HIP-event timing of mdfit_fit_batch (mdfit_profile_enable):
 // per call, events around the whole call and around fit_kernel, on the
 // caller's stream
@@ -861,10 +777,15 @@ void mdfit_default_opts(mdfit_opts* o) {
   o->seed = 0;
   o->num_warmup = 500;
   o->num_samples = 1000;
+  o->index_base = 0;
 }
 
-int64_t mdfit_workspace_bytes(int64_t n_taxa) {
+int64_t mdfit_workspace_bytes(int64_t n_taxa, const mdfit_opts* opts) {
   if (n_taxa < 0) return 0;
+  mdfit_opts o;
+  mdfit_default_opts(&o);
+  if (opts) o = *opts;
+  if (o.mode == MDFIT_MODE_NUTS) return mdfit::nuts::workspace_bytes(n_taxa, o.num_samples);
   const int64_t b = 4 * (mdfit::kWsRing + 2 * n_taxa);
   return (b + 255) / 256 * 256;
 }
@@ -879,14 +800,21 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   mdfit_opts o;
   mdfit_default_opts(&o);
   if (opts) o = *opts;
-  if (o.mode != MDFIT_MODE_MAP) return set_err(MDFIT_E_ARG, "unsupported mode");
+  if (o.mode != MDFIT_MODE_MAP && o.mode != MDFIT_MODE_NUTS) return set_err(MDFIT_E_ARG, "unsupported mode");
   if (o.max_iter < 1) return set_err(MDFIT_E_ARG, "max_iter < 1");
   if (n_taxa > ((int64_t)1 << 29)) return set_err(MDFIT_E_ARG, "n_taxa exceeds 2^29 per call");
   hipStream_t s = (hipStream_t)hip_stream;
   int* ws = (int*)workspace;
   prof_record(0, s);
-  if (hipMemsetAsync(ws, 0, (size_t)mdfit_workspace_bytes(n_taxa), s) != hipSuccess)
+  if (hipMemsetAsync(ws, 0, (size_t)(o.mode == MDFIT_MODE_NUTS ? 256 : mdfit_workspace_bytes(n_taxa, &o)), s) !=
+      hipSuccess)
     return check_launch("hipMemsetAsync(workspace)");
+  if (o.mode == MDFIT_MODE_NUTS) {
+    if (int rc = mdfit::nuts::fit_batch(y, N, mm, n_taxa, o, out, pred, status, workspace, s)) return rc;
+    prof_record(3, s);
+    if (g_prof.on && g_prof.n < kProfMax) ++g_prof.n;
+    return 0;
+  }
   const int64_t n_init = MDFIT_NSUBFIT * n_taxa;
   hipLaunchKernelGGL(mdfit::init_kernel, dim3((unsigned)((n_init + 255) / 256)), dim3(256), 0, s, y, N,
                      n_taxa, out);
@@ -950,6 +878,13 @@ int mdfit_set_stamp(unsigned long long* buf) {
   return 0;
 }
 #endif
+
+int mdfit_nuts_potential(const int32_t* model, const int32_t* subset, const uint32_t* y, const uint32_t* N,
+                         const double* v, int64_t n, double* U, double* g, void* hip_stream) {
+  if (n < 0 || (n > 0 && (!model || !subset || !y || !N || !v || !U || !g)))
+    return set_err(MDFIT_E_ARG, "bad arguments");
+  return mdfit::nuts::potential(model, subset, y, N, v, n, U, g, (hipStream_t)hip_stream);
+}
 
 const char* mdfit_last_error(void) { return g_err; }
 

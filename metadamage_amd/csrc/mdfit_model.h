@@ -390,4 +390,88 @@ __device__ __forceinline__ void newton_dir(bool pmd, const double u[4], const do
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// record pieces shared by the MAP and sampling assembly kernels (one wave per
+// taxon, counts staged in LDS)
+// ---------------------------------------------------------------------------
+// sums (fits.py:272-283) and noise (fits.py:359-376) into the record s_rec
+__device__ __forceinline__ void record_sums_noise(int lane, const double* s_y, const double* s_N,
+                                                  const uint32_t* s_mm, bool has_mm, double* s_rec) {
+  // ---- sums (fits.py:272-283) -------------------------------------------------
+  {
+    const double v = lane < kNPos ? 1.0 : 0.0;
+    const double fw = lane < kNHalf ? 1.0 : 0.0;
+    const int pi = lane < kNPos ? lane : 0;
+    const double yv = v * s_y[pi], nv = v * s_N[pi];
+    const double nf = gsum<64>(fw * nv), nt = gsum<64>(nv);
+    const double yf = gsum<64>(fw * yv), yt = gsum<64>(yv);
+    if (lane == 0) {
+      s_rec[MDFIT_F_N_Z1_FORWARD] = s_N[0];
+      s_rec[MDFIT_F_N_Z1_REVERSE] = s_N[kNHalf];
+      s_rec[MDFIT_F_N_SUM_FORWARD] = nf;
+      s_rec[MDFIT_F_N_SUM_REVERSE] = nt - nf;
+      s_rec[MDFIT_F_N_SUM_TOTAL] = nt;
+      s_rec[MDFIT_F_Y_SUM_FORWARD] = yf;
+      s_rec[MDFIT_F_Y_SUM_REVERSE] = yt - yf;
+      s_rec[MDFIT_F_Y_SUM_TOTAL] = yt;
+    }
+  }
+
+  // ---- noise (fits.py:359-376) -------------------------------------------------
+  {
+    // lane j < 12 owns mismatch column j (AC AG AT CA CG CT GA GC GT TA TC TG);
+    // CT is NaN on rows 0..14, GA on rows 15..29.
+    const int j = lane < kNMM ? lane : 0;
+    const bool own = lane < kNMM && has_mm;
+    double s = 0.0, cnt = 0.0;
+    for (int i = 0; i < kNPos; ++i) {
+      const bool nanned = (j == 5 && i < kNHalf) || (j == 6 && i >= kNHalf);
+      if (!nanned) {
+        s += (double)s_mm[i * kNMM + j];
+        cnt += 1.0;
+      }
+    }
+    const double m = s / cnt;
+    double sa[3] = {0, 0, 0}, ca[3] = {0, 0, 0};
+    for (int i = 0; i < kNPos; ++i) {
+      const bool nanned = (j == 5 && i < kNHalf) || (j == 6 && i >= kNHalf);
+      const double x = (double)s_mm[i * kNMM + j] / m;
+      if (own && !nanned && !isnan(x)) {
+        const int h = i < kNHalf ? 1 : 2;
+        sa[0] += x;
+        ca[0] += 1.0;
+        sa[h] += x;
+        ca[h] += 1.0;
+      }
+    }
+    double mean[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) mean[q] = gsum<16>(sa[q]) / gsum<16>(ca[q]);
+    double ss[3] = {0, 0, 0};
+    for (int i = 0; i < kNPos; ++i) {
+      const bool nanned = (j == 5 && i < kNHalf) || (j == 6 && i >= kNHalf);
+      const double x = (double)s_mm[i * kNMM + j] / m;
+      if (own && !nanned && !isnan(x)) {
+        const int h = i < kNHalf ? 1 : 2;
+        ss[0] += (x - mean[0]) * (x - mean[0]);
+        ss[h] += (x - mean[h]) * (x - mean[h]);
+      }
+    }
+    double nz[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const double c = gsum<16>(ca[q]);
+      nz[q] = c > 0.0 ? sqrt(gsum<16>(ss[q]) / c) : NAN;
+    }
+    if (lane == 0) {
+      const bool have = has_mm;
+      s_rec[MDFIT_F_NORMALIZED_NOISE] = have ? nz[0] : NAN;
+      s_rec[MDFIT_F_NORMALIZED_NOISE_FORWARD] = have ? nz[1] : NAN;
+      s_rec[MDFIT_F_NORMALIZED_NOISE_REVERSE] = have ? nz[2] : NAN;
+    }
+  }
+
+}
+
 }  // namespace mdfit

@@ -1,0 +1,1038 @@
+// mdfit_nuts.hip — MI355X (gfx950) sampling mode: MDFIT-NUTS v1.
+//
+// The reference samples every sub-fit with numpyro NUTS (fits.py:382-387,
+// num_warmup 500 / num_samples 1000, one chain) and post-processes the draws
+// (fits.py:89-172, 230-356).  Two launches:
+//
+//   nuts_chain_kernel  persistent, the MAP kernel's lane layout: a wave = 2
+//                      groups of 32 lanes, a group = 2 rows of 16, lane =
+//                      position (lane 15 of a row a pad).  A group runs one
+//                      all-position chain (rows' sums added, identical state)
+//                      or the forward/reverse pair of one model (a chain per
+//                      row).  Every trip every running chain does ONE
+//                      potential + gradient evaluation -- a leapfrog step, an
+//                      initial-point probe or a step-size-search step -- and
+//                      then advances its state machine (iterative NUTS tree,
+//                      Stan-window adaptation).  Kept draws go to the
+//                      workspace: double[T][6][S][4] = (q, A, c, phi).
+//   nuts_post_kernel   one wave per taxon, lanes over draws: pointwise
+//                      log-likelihood -> lppd / pWAIC / waic_i, n_sigma x3,
+//                      asymmetry, posterior means, predictive Beta-Binomial
+//                      draws -> median / 68 % HPDI by a bitonic sort in LDS,
+//                      sums, noise.
+//
+// Same algorithm and the same Philox4x32-10 streams as oracle/mdfit_nuts.c
+// (written separately; see its header for the counter layout), so GPU chains
+// follow the oracle's draw for draw until a floating-point difference flips
+// a decision.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "../../include/mdfit.h"
+#include "mdfit_host.h"
+#include "mdfit_model.h"
+#include "mdfit_special.h"
+
+namespace mdfit::nuts {
+
+constexpr int kMaxDepth = 10;
+constexpr double kMaxDelta = 1000.0;
+constexpr double kTarget = 0.8;
+constexpr double kTiny = 2.2250738585072014e-308;
+constexpr double kHuge = 1.7976931348623157e308;
+constexpr int kMaxSamples = 4096;  // LDS bound of the post kernel
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 and the draw helpers (oracle: philox4x32, nuniform, nnormal)
+// ---------------------------------------------------------------------------
+struct Stream {
+  uint32_t k0, k1, c0, c1;
+};
+
+__device__ __forceinline__ Stream make_stream(uint64_t seed, int64_t g, int sub) {
+  Stream s;
+  s.k0 = (uint32_t)seed;
+  s.k1 = (uint32_t)(seed >> 32);
+  s.c0 = (uint32_t)(uint64_t)g;
+  s.c1 = (uint32_t)((uint64_t)g >> 32) + ((uint32_t)sub << 24);
+  return s;
+}
+
+__device__ __forceinline__ uint4 block(const Stream& s, uint32_t w2, uint32_t w3) {
+  uint32_t c0 = s.c0, c1 = s.c1, c2 = w2, c3 = w3, k0 = s.k0, k1 = s.k1;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return make_uint4(c0, c1, c2, c3);
+}
+
+__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {  // [0, 1)
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+__device__ __forceinline__ double uniform(const Stream& s, uint32_t w2, uint32_t w3) {
+  const uint4 o = block(s, w2, w3);
+  return u53(o.x, o.y);
+}
+
+__device__ __forceinline__ double normal(const Stream& s, uint32_t w2, uint32_t w3) {
+  const uint4 o = block(s, w2, w3);
+  const double u1 = 1.0 - u53(o.x, o.y), u2 = u53(o.z, o.w);
+  return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+}
+
+__device__ __forceinline__ double sel4(const double v[4], int j) {
+  return j == 0 ? v[0] : (j == 1 ? v[1] : (j == 2 ? v[2] : v[3]));
+}
+
+__device__ __forceinline__ bool active(bool pmd, int j) { return pmd || j == 0 || j == 3; }
+
+// ---------------------------------------------------------------------------
+// potential (oracle: nuts_potential), row-collective
+// ---------------------------------------------------------------------------
+struct Pot {
+  double U;
+  double g[4];
+};
+
+// -(log density + log|J|) of the row's (or, `whole`, the group's) points at
+// v and its gradient.  Lanes 0-2 of a row resolve sigmoid(v0..v2), lane 3
+// exp(v3); the phi triple is the pad lane's lg(0 + phi).
+__device__ __forceinline__ Pot potential(const PointData& pd, const double v[4], bool whole) {
+  const int i = (int)(threadIdx.x & 15);
+  const double x = i < 3 ? sel4(v, i) : v[3];
+  const double e = exp(i < 3 ? -fabs(x) : x);
+  const double sp = flog1p(e);
+  const double rr = rcp(1.0 + e);
+  const bool pos = x >= 0.0;
+  const double p = pos ? rr : e * rr, omp = pos ? e * rr : rr;
+  const double lp = pos ? -sp : x - sp, l1p = pos ? -(x + sp) : -sp;
+  // prior + log|J|: q, A ~ Beta(2,3) -> 2 ln p + 3 ln(1-p); c ~ Beta(1,9) -> ln c + 9 ln(1-c)
+  const double pr = i == 2 ? lp + 9.0 * l1p : 2.0 * lp + 3.0 * l1p;
+  const double q = rowb<0>(p), omq = rowb<0>(omp), prq = rowb<0>(pr);
+  const double A0 = rowb<1>(p), omA = rowb<1>(omp), prA = rowb<1>(pr);
+  const double c0 = rowb<2>(p), omc = rowb<2>(omp), prc = rowb<2>(pr);
+  const double delta = rowb<3>(e);
+  const double phi = delta + 2.0;
+  const bool pmd = pd.pmd;
+  const double A = pmd ? A0 : 0.0, c = pmd ? c0 : 0.0;
+  double lprior = prq + v[3] - delta / 1000.0;
+  if (pmd) lprior += prA + prc;
+
+  double D, dq, dA;
+  if (pmd) {
+    const double w = powk(omq, pd.k);
+    D = fma(A, w, c);
+    dq = pd.k > 0 ? -A * (double)pd.k * (w * rcp(omq)) : 0.0;
+    dA = w;
+  } else {
+    D = q;
+    dq = 1.0;
+    dA = 0.0;
+  }
+  const bool bad_lane = (pd.valid && !(D < 1.0)) || (pmd && A + c >= 1.0);
+  const double a = D * phi, b = (1.0 - D) * phi;
+  const LG3 t1 = lg3<false>(pd.y + a);
+  const LG3 t4 = lg3<false>(a);
+  const double la = t1.l - t4.l, Pa = t1.p - t4.p;
+  const LG3 t2 = lg3<false>(pd.N - pd.y + b);
+  const LG3 t5 = lg3<false>(b);
+  const double lb = t2.l - t5.l, Pb = t2.p - t5.p;
+  const LG3 t3 = lg3<false>(pd.N + phi);
+  const double t6l = rowb<15>(t3.l), t6p = rowb<15>(t3.p);  // pad lane: lg(0 + phi)
+  const double ell = (la + lb) - (t3.l - t6l);
+  const double lD = phi * (Pa - Pb);
+  const double lF = D * Pa + (1.0 - D) * Pb + (t6p - t3.p);
+  double acc[5] = {ell, lD * dq, lD * dA, lD, lF};
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const double s16 = gsum<16>(pd.valid ? acc[j] : 0.0);
+    acc[j] = whole ? s16 + __shfl_xor(s16, 16, 64) : s16;
+  }
+  const unsigned long long bm = __ballot(bad_lane);
+  const int sh = (int)(threadIdx.x & (whole ? ~31 : ~15));
+  const bool bad = ((bm >> sh) & (whole ? 0xFFFFFFFFull : 0xFFFFull)) != 0ull;
+  Pot o;
+  o.U = -(acc[0] + lprior);
+  o.g[0] = -(acc[1] * (q * omq) + (2.0 - 5.0 * q));
+  o.g[1] = pmd ? -(acc[2] * (A * omA) + (2.0 - 5.0 * A)) : 0.0;
+  o.g[2] = pmd ? -(acc[3] * (c * omc) + (1.0 - 10.0 * c)) : 0.0;
+  o.g[3] = -(acc[4] * delta + (1.0 - delta / 1000.0));
+  if (bad || !isfinite(o.U)) {
+    o.U = INFINITY;
+    o.g[0] = o.g[1] = o.g[2] = o.g[3] = 0.0;
+  }
+  return o;
+}
+
+// ---------------------------------------------------------------------------
+// adaptation schedule (oracle: adapt_windows) -- end of window w, or -1
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void windows(int nw, int w, int* end_w, int* nwin) {
+  int n = 0, e = -1;
+  if (nw < 20) {
+    *end_w = w == 0 ? nw - 1 : -1;
+    *nwin = 1;
+    return;
+  }
+  int init_buffer = 75, term_buffer = 50, base_window = 25;
+  if (nw < init_buffer + term_buffer + base_window) {
+    init_buffer = (int)(0.15 * nw);
+    term_buffer = (int)(0.1 * nw);
+    base_window = nw - init_buffer - term_buffer;
+  }
+  if (w == n) e = init_buffer - 1;
+  n++;
+  const int end_start = nw - term_buffer;
+  int next_size = base_window, next_start = init_buffer;
+  while (next_start < end_start && n < 15) {
+    const int cs = next_start;
+    int csz = next_size;
+    if (3 * csz <= end_start - cs) next_size = 2 * csz;
+    else csz = end_start - cs;
+    next_start = cs + csz;
+    if (w == n) e = next_start - 1;
+    n++;
+  }
+  if (w == n) e = nw - 1;
+  *end_w = e;
+  *nwin = n + 1;
+}
+
+// checkpoint index range of leaf n (oracle: ckpt_idxs)
+__device__ __forceinline__ void ckpt_idxs(int n, int* imin, int* imax) {
+  const int mx = __popc((unsigned)(n >> 1));
+  const int ns = __builtin_ctz(~(unsigned)n);  // trailing ones
+  *imax = mx;
+  *imin = mx - ns + 1;
+}
+
+__device__ __forceinline__ double logaddexp(double a, double b) {
+  const double m = fmax(a, b);
+  return m == -INFINITY ? -INFINITY : m + log1p(exp(-fabs(a - b)));
+}
+
+__device__ __forceinline__ bool is_turning(bool pmd, const double invm[4], const double rl[4], const double rr[4],
+                                           const double rsum[4]) {
+  double dl = 0.0, dr = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!active(pmd, j)) continue;
+    const double rs = rsum[j] - 0.5 * (rl[j] + rr[j]);
+    dl += invm[j] * rl[j] * rs;
+    dr += invm[j] * rr[j] * rs;
+  }
+  return dl <= 0.0 || dr <= 0.0;
+}
+
+__device__ __forceinline__ double kinetic(bool pmd, const double invm[4], const double r[4]) {
+  double k = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (active(pmd, j)) k += invm[j] * r[j] * r[j];
+  return 0.5 * k;
+}
+
+// cold per-chain state (one slot per 16-lane row; every lane of the row
+// writes the same values)
+struct RowState {
+  double lz[4], lr[4], lg[4];  // left end of the trajectory
+  double rz[4], rr[4], rg[4];  // right end
+  double tz[4], tg[4], tpe;    // proposal of the tree = the chain's current state
+  double sz[4], sg[4], spe;    // proposal of the subtree being built
+  double wmean[4], wm2[4];     // Welford (slow windows)
+};
+
+constexpr int kInit = 1, kFind = 2, kIter = 3, kDone = 4;
+
+// ---------------------------------------------------------------------------
+// chain kernel
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kWave) void nuts_chain_kernel(const uint32_t* __restrict__ gy,
+                                                           const uint32_t* __restrict__ gN, int64_t T,
+                                                           mdfit_opts o, double* __restrict__ out,
+                                                           int* __restrict__ ws, double* __restrict__ samples) {
+  __shared__ RowState srow[4];
+  const int lane = threadIdx.x;
+  const int r = lane & 31, h = r >> 4, i = r & 15, row = lane >> 4;
+  const int leader = lane & ~31;
+  const int qi = blockIdx.x % kQueues;
+  const int64_t ntask = 4 * T;  // [0,2T) all-position chains, [2T,4T) fwd/rev pairs
+  const int64_t qlo = ntask * qi / kQueues, qhi = ntask * (qi + 1) / kQueues;
+  const int W = o.num_warmup, S = o.num_samples;
+  RowState& R = srow[row];
+
+  PointData pd;
+  pd.valid = i < kNHalf;
+  pd.k = pd.valid ? i : 0;
+  pd.y = pd.N = 0.0;
+  pd.pmd = true;
+
+  // task / chain bookkeeping (row-uniform; identical on both rows of a whole chain)
+  int mode = 0;  // 0 idle, kInit, kFind, kIter, kDone
+  bool whole = false, drained = false;
+  int64_t taxon = 0;
+  int sub = 0;
+  Stream st = make_stream(0, 0, 0);
+  int it = 0, attempt = 0;
+  // dynamics
+  double pz[4] = {0, 0, 0, 0}, pr[4] = {0, 0, 0, 0}, pg[4] = {0, 0, 0, 0};
+  double step = 0.0, eps = 1.0, e0 = 0.0;
+  double invm[4] = {1, 1, 1, 1};
+  // step-size search
+  int f_call = 0, f_m = 0, f_last = 0, f_dir = 0;
+  // dual averaging, windows
+  double x_avg = 0.0, g_avg = 0.0, mu = 0.0;
+  int t_da = 0, widx = 0, wn = 0;
+  // tree
+  double t_w = 0.0, t_rsum[4] = {0, 0, 0, 0}, t_acc = 0.0, u_tr = 0.0;
+  int t_n = 0, t_depth = 0, leaf_ctr = 0, nleap = 0;
+  bool t_turn = false, t_div = false, right = true;
+  // subtree
+  double s_w = 0.0, s_rsum[4] = {0, 0, 0, 0}, s_acc = 0.0;
+  int s_n = 0, n_leaf = 0, nmax = 1;
+  bool s_div = false;
+  // checkpoints: lane i < kMaxDepth of the row holds checkpoint i
+  double ck_r[4] = {0, 0, 0, 0}, ck_rs[4] = {0, 0, 0, 0};
+  // statistics of the kept iterations
+  double st_div = 0.0, st_leap = 0.0;
+
+  while (true) {
+    // ---- 1. free groups start a task (one atomic per wave-trip) --------------
+    const unsigned long long busy_m = __ballot(mode != 0 && mode != kDone);
+    const bool group_free = ((busy_m >> leader) & 0xFFFFFFFFull) == 0ull;
+    if (group_free) mode = 0;  // both chains finished (or none started)
+    const bool need = group_free && !drained;
+    bool starting = false;
+    if (__any(need)) {
+      const unsigned long long m = __ballot(need && r == 0);
+      int base = 0;
+      if (lane == 0) base = atomicAdd(ws + qi, __popcll(m));
+      base = __shfl(base, 0);
+      if (need) {
+        const int64_t task = qlo + base + __popcll(m & ((1ull << leader) - 1ull));
+        if (task >= qhi) {
+          drained = true;
+          mode = 0;
+        } else {
+          whole = task < 2 * T;
+          if (whole) {
+            sub = task < T ? 0 : 1;
+            taxon = task - (sub ? T : 0);
+          } else {
+            const int64_t pt = task - 2 * T;
+            const bool pmdm = pt < T;
+            taxon = pmdm ? pt : pt - T;
+            sub = (pmdm ? 2 : 4) + h;
+          }
+          starting = true;
+        }
+      }
+    }
+    if (starting) {
+      pd.pmd = sub == 0 || sub == 2 || sub == 3;
+      // row h reads columns h*15 + k: the two halves of an all-position chain,
+      // or the forward (sub 2 / 4) / reverse (sub 3 / 5) chain of a pair
+      const int colv = pd.valid ? h * kNHalf + pd.k : 0;
+      pd.y = pd.valid ? (double)gy[taxon * kLD + colv] : 0.0;
+      pd.N = pd.valid ? (double)gN[taxon * kLD + colv] : 0.0;
+      st = make_stream(o.seed, o.index_base + taxon, sub);
+      // fresh chain state (oracle: nuts_chain)
+      mode = kInit;
+      attempt = 0;
+      it = 0;
+      st_div = st_leap = 0.0;
+      eps = 1.0;
+      step = 0.0;
+      f_call = f_m = f_last = f_dir = 0;
+      x_avg = g_avg = mu = 0.0;
+      t_da = widx = wn = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pz[j] = active(pd.pmd, j) ? -2.0 + 4.0 * uniform(st, 0xFFFF0000u, (uint32_t)j) : 0.0;
+        pr[j] = pg[j] = 0.0;
+        invm[j] = 1.0;
+        R.wmean[j] = R.wm2[j] = 0.0;
+      }
+    }
+    if (!__any(mode != 0 || !drained)) break;
+    const bool running = mode == kInit || mode == kFind || mode == kIter;
+    if (!__any(running)) continue;  // (only finished chains of unfinished groups)
+
+    // ---- 2. one evaluation: the initial point, or a leapfrog step ------------
+    double rh[4], zev[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      rh[j] = pr[j] - 0.5 * step * pg[j];
+      zev[j] = mode == kInit ? pz[j] : pz[j] + step * invm[j] * rh[j];
+    }
+    const Pot P = potential(pd, zev, whole);
+    if (!running) continue;
+    double rn[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      rn[j] = rh[j] - 0.5 * step * P.g[j];
+      pz[j] = zev[j];
+    }
+
+    bool begin_iter = false, begin_find = false;
+    if (mode == kInit) {
+      if (isfinite(P.U)) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          R.tz[j] = zev[j];
+          R.tg[j] = P.g[j];
+        }
+        R.tpe = P.U;
+        eps = 1.0;
+        f_call = 0;
+        begin_find = true;
+      } else if (++attempt >= 100) {
+        // no finite initial point: NaN draws, status 2
+        for (int s = i; s < S; s += 16)
+          if (!whole || h == 0)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              samples[((taxon * MDFIT_NSUBFIT + sub) * (int64_t)S + s) * 4 + j] = NAN;
+        if ((!whole || h == 0) && i < 4) {
+          double* dg = out + taxon * MDFIT_NOUT + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * sub;
+          dg[4 + i] = i == 2 ? (double)MDFIT_NONFINITE : NAN;
+        }
+        mode = kDone;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          pz[j] = active(pd.pmd, j) ? -2.0 + 4.0 * uniform(st, 0xFFFF0000u + (uint32_t)attempt, (uint32_t)j) : 0.0;
+      }
+    } else if (mode == kFind) {
+      const double de = (P.U + kinetic(pd.pmd, invm, rn)) - e0;
+      const int dnew = log(kTarget) < -de ? 1 : -1;
+      f_last = f_dir;
+      f_dir = dnew;
+      ++f_m;
+      const bool cont = (eps > kTiny || f_dir >= 0) && (eps < kHuge || f_dir <= 0) &&
+                        (f_last == 0 || f_dir == f_last) && f_m < 4000;
+      if (cont) {
+        begin_find = true;  // next probe of the same search
+      } else {
+        mu = log(10.0 * eps);
+        x_avg = g_avg = 0.0;
+        t_da = 0;
+        begin_iter = true;
+      }
+    } else {  // kIter: a leaf of the subtree
+      ++nleap;
+      double de = (P.U + kinetic(pd.pmd, invm, rn)) - e0;
+      if (isnan(de)) de = INFINITY;
+      const double w = -de;
+      const bool dv = de > kMaxDelta;
+      const double acc = de > 0.0 ? exp(-de) : 1.0;
+      if (n_leaf == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          R.sz[j] = zev[j];
+          R.sg[j] = P.g[j];
+          s_rsum[j] = rn[j];
+        }
+        R.spe = P.U;
+        s_w = w;
+        s_acc = acc;
+        s_n = 1;
+      } else {
+        const double nw = logaddexp(s_w, w);
+        const double prob = exp(w - nw);
+        if (uniform(st, (uint32_t)it, 32u + (uint32_t)leaf_ctr) < prob) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            R.sz[j] = zev[j];
+            R.sg[j] = P.g[j];
+          }
+          R.spe = P.U;
+        }
+        s_w = nw;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s_rsum[j] += rn[j];
+        s_acc += acc;
+        s_n += 1;
+      }
+      s_div = dv;
+      ++leaf_ctr;
+      int imin, imax;
+      ckpt_idxs(n_leaf, &imin, &imax);
+      if ((n_leaf & 1) == 0 && i == imax) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          ck_r[j] = rn[j];
+          ck_rs[j] = s_rsum[j];
+        }
+      }
+      bool my_turn = false;
+      if (i >= imin && i <= imax) {
+        double sub_rsum[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sub_rsum[j] = s_rsum[j] - ck_rs[j] + ck_r[j];
+        my_turn = is_turning(pd.pmd, invm, ck_r, rn, sub_rsum);
+      }
+      const unsigned long long tm = __ballot(my_turn);
+      const bool s_turn = ((tm >> (lane & ~15)) & 0xFFFFull) != 0ull;
+      ++n_leaf;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pr[j] = rn[j];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pg[j] = P.g[j];
+      if (s_turn || s_div || n_leaf == nmax) {
+        // merge the subtree into the tree: biased progressive sampling
+        const double prob = (s_turn || s_div) ? 0.0 : fmin(1.0, exp(s_w - t_w));
+        if (u_tr < prob) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            R.tz[j] = R.sz[j];
+            R.tg[j] = R.sg[j];
+          }
+          R.tpe = R.spe;
+        }
+        double olr[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          olr[j] = right ? R.lr[j] : R.rr[j];  // r of the untouched end
+          if (right) {
+            R.rz[j] = pz[j];
+            R.rr[j] = pr[j];
+            R.rg[j] = pg[j];
+          } else {
+            R.lz[j] = pz[j];
+            R.lr[j] = pr[j];
+            R.lg[j] = pg[j];
+          }
+        }
+        t_w = logaddexp(t_w, s_w);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t_rsum[j] += s_rsum[j];
+        t_turn = s_turn || (right ? is_turning(pd.pmd, invm, olr, pr, t_rsum) : is_turning(pd.pmd, invm, pr, olr, t_rsum));
+        t_div = s_div;
+        t_acc += s_acc;
+        t_n += s_n;
+        ++t_depth;
+        if (t_depth >= kMaxDepth || t_turn || t_div) {
+          // ---- the transition is complete: adapt or keep the draw ----------
+          const double accp = t_acc / (double)t_n;
+          if (it < W) {
+            ++t_da;
+            const double gg = kTarget - accp;
+            g_avg = (1.0 - 1.0 / (t_da + 10.0)) * g_avg + gg / (t_da + 10.0);
+            const double x_t = mu - sqrt((double)t_da) / 0.05 * g_avg;
+            const double wt = pow((double)t_da, -0.75);
+            x_avg = (1.0 - wt) * x_avg + wt * x_t;
+            eps = exp(it == W - 1 ? x_avg : x_t);
+            if (eps < kTiny) eps = kTiny;
+            int wend, nwin;
+            windows(W, widx, &wend, &nwin);
+            const bool middle = widx > 0 && widx < nwin - 1;
+            if (middle) {
+              ++wn;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                if (!active(pd.pmd, j)) continue;
+                const double d0 = R.tz[j] - R.wmean[j];
+                R.wmean[j] += d0 / wn;
+                R.wm2[j] += d0 * (R.tz[j] - R.wmean[j]);
+              }
+            }
+            const bool at_end = it == wend;
+            if (at_end && middle) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                if (!active(pd.pmd, j)) continue;
+                const double var = R.wm2[j] / (wn - 1);
+                invm[j] = ((double)wn / (wn + 5.0)) * var + 1e-3 * (5.0 / (wn + 5.0));
+                R.wmean[j] = R.wm2[j] = 0.0;
+              }
+              wn = 0;
+              ++f_call;
+              begin_find = true;
+            }
+            if (at_end) ++widx;
+          } else {
+            const int64_t sidx = ((taxon * MDFIT_NSUBFIT + sub) * (int64_t)S + (it - W)) * 4;
+            if ((!whole || h == 0) && i < 4) {
+              const double zj = R.tz[i];
+              samples[sidx + i] = i == 3 ? exp(zj) + 2.0
+                                         : ((i == 0 || pd.pmd) ? 1.0 / (1.0 + exp(-zj)) : 0.0);
+            }
+            st_div += t_div ? 1.0 : 0.0;
+            st_leap += (double)nleap;
+          }
+          ++it;
+          if (it == W + S) {
+            if ((!whole || h == 0) && i < 4) {
+              double* dg = out + taxon * MDFIT_NOUT + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * sub;
+              dg[4 + i] = i == 0 ? eps : (i == 1 ? st_leap / S : (i == 2 ? (double)MDFIT_OK : st_div));
+            }
+            mode = kDone;
+          } else if (!begin_find) {
+            begin_iter = true;
+          }
+        } else {
+          // next doubling
+          const int j = t_depth;
+          right = (block(st, (uint32_t)it, 4u + 2u * (uint32_t)j).x & 1u) != 0u;
+          u_tr = uniform(st, (uint32_t)it, 5u + 2u * (uint32_t)j);
+          n_leaf = 0;
+          nmax = 1 << j;
+          step = right ? eps : -eps;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            pz[k] = right ? R.rz[k] : R.lz[k];
+            pr[k] = right ? R.rr[k] : R.lr[k];
+            pg[k] = right ? R.rg[k] : R.lg[k];
+          }
+        }
+      } else {
+        step = right ? eps : -eps;  // next leaf of the subtree continues from (pz, pr, pg)
+      }
+    }
+
+    if (begin_find) {
+      // one probe of find_reasonable_step_size from the current state
+      if (mode != kFind || f_m == 0) {
+        f_m = 0;
+        f_last = f_dir = 0;
+      }
+      if (mode != kFind) mode = kFind;
+      eps = ldexp(eps, f_dir);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pr[j] = active(pd.pmd, j)
+                    ? normal(st, 0xFFFE0000u + 4096u * (uint32_t)f_call + (uint32_t)f_m, (uint32_t)j) * sqrt(1.0 / invm[j])
+                    : 0.0;
+        pz[j] = R.tz[j];
+        pg[j] = R.tg[j];
+      }
+      e0 = R.tpe + kinetic(pd.pmd, invm, pr);
+      step = eps;
+    }
+    if (begin_iter) {
+      mode = kIter;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pr[j] = active(pd.pmd, j) ? normal(st, (uint32_t)it, (uint32_t)j) * sqrt(1.0 / invm[j]) : 0.0;
+        pz[j] = R.tz[j];
+        pg[j] = R.tg[j];
+        R.lz[j] = R.rz[j] = pz[j];
+        R.lr[j] = R.rr[j] = pr[j];
+        R.lg[j] = R.rg[j] = pg[j];
+        t_rsum[j] = pr[j];
+      }
+      e0 = R.tpe + kinetic(pd.pmd, invm, pr);
+      t_w = 0.0;
+      t_acc = 0.0;
+      t_n = 0;
+      t_depth = 0;
+      t_turn = t_div = false;
+      leaf_ctr = 0;
+      nleap = 0;
+      right = (block(st, (uint32_t)it, 4u).x & 1u) != 0u;
+      u_tr = uniform(st, (uint32_t)it, 5u);
+      n_leaf = 0;
+      nmax = 1;
+      step = right ? eps : -eps;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// post kernel: one wave per taxon
+// ---------------------------------------------------------------------------
+// frac = obs / N of one predictive Beta-Binomial draw (oracle: predictive_frac)
+struct Draw {
+  const Stream* st;
+  uint32_t w2, w3;
+  __device__ double uni() { return uniform(*st, w2, w3++); }
+  __device__ double nrm() { return normal(*st, w2, w3++); }
+};
+
+__device__ double log_gamma_draw(Draw& d, double alpha) {
+  double boost = 0.0;
+  if (alpha < 1.0) {
+    boost = log(1.0 - d.uni()) / alpha;
+    alpha += 1.0;
+  }
+  const double dd = alpha - 1.0 / 3.0, cc = 1.0 / sqrt(9.0 * dd);
+  for (int k = 0; k < 256; ++k) {
+    const double x = d.nrm();
+    double v = 1.0 + cc * x;
+    if (v <= 0.0) continue;
+    v = v * v * v;
+    const double u = d.uni();
+    if (u < 1.0 - 0.0331 * x * x * x * x) return log(dd * v) + boost;
+    if (log(u) < 0.5 * x * x + dd * (1.0 - v + log(v))) return log(dd * v) + boost;
+  }
+  return log(dd) + boost;
+}
+
+__device__ double binomial_draw(Draw& d, double n, double p) {
+  if (n <= 0.0 || p <= 0.0) return 0.0;
+  if (p >= 1.0) return n;
+  const bool flip = p > 0.5;
+  const double pp = flip ? 1.0 - p : p, qq = 1.0 - pp;
+  double k;
+  if (n * pp < 10.0) {
+    const double u = d.uni();
+    double pmf = exp(n * log1p(-pp)), cdf = pmf;
+    k = 0.0;
+    const double ratio = pp / qq;
+    while (u > cdf && k < n && k < 10000.0) {
+      pmf *= (n - k) / (k + 1.0) * ratio;
+      k += 1.0;
+      cdf += pmf;
+    }
+  } else {
+    const double spq = sqrt(n * pp * qq), bb = 1.15 + 2.53 * spq;
+    const double aa = -0.0873 + 0.0248 * bb + 0.01 * pp, cc = n * pp + 0.5;
+    const double vr = 0.92 - 4.2 / bb, alpha = (2.83 + 5.1 / bb) * spq;
+    const double lpq = log(pp / qq), m = floor((n + 1.0) * pp);
+    const double hh = lgamma(m + 1.0) + lgamma(n - m + 1.0);
+    k = floor(cc);
+    for (int it = 0; it < 256; ++it) {
+      const double u = d.uni() - 0.5, v = d.uni();
+      const double us = 0.5 - fabs(u);
+      const double kk = floor((2.0 * aa / us + bb) * u + cc);
+      if (kk < 0.0 || kk > n) continue;
+      if (us >= 0.07 && v <= vr) {
+        k = kk;
+        break;
+      }
+      const double lv = log(v * alpha / (aa / (us * us) + bb));
+      if (lv <= hh - lgamma(kk + 1.0) - lgamma(n - kk + 1.0) + (kk - m) * lpq) {
+        k = kk;
+        break;
+      }
+    }
+  }
+  return flip ? n - k : k;
+}
+
+__device__ __forceinline__ double d_at(const double* th, bool pmd, int k) {
+  double D = pmd ? th[1] * pow(1.0 - th[0], (double)k) + th[2] : th[0];
+  return D < 0.0 ? 0.0 : (D > 1.0 ? 1.0 : D);
+}
+
+__device__ double predictive_frac(const Stream& st, int s, int col, int k, double Nn, const double* th) {
+  const double D = d_at(th, true, k);
+  Draw d{&st, 0xFFFD0000u + (uint32_t)s, (uint32_t)col << 16};
+  const double lx = log_gamma_draw(d, D * th[3]), ly = log_gamma_draw(d, (1.0 - D) * th[3]);
+  const double p = 1.0 / (1.0 + exp(ly - lx));
+  return binomial_draw(d, Nn, p) / Nn;
+}
+
+// wave-wide reductions
+__device__ __forceinline__ double wsum(double v) { return gsum<64>(v); }
+__device__ __forceinline__ double wmax(double v) {
+  for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// bitonic sort of n <= kMaxSamples doubles in LDS (n padded to a power of two with +inf)
+__device__ void lds_sort(double* v, int n) {
+  int m = 1;
+  while (m < n) m <<= 1;
+  for (int j = n + threadIdx.x; j < m; j += kWave) v[j] = INFINITY;
+  __syncthreads();
+  for (int k = 2; k <= m; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int x = threadIdx.x; x < m; x += kWave) {
+        const int y = x ^ j;
+        if (y > x) {
+          const double a = v[x], b = v[y];
+          const bool up = (x & k) == 0;
+          if ((a > b) == up) {
+            v[x] = b;
+            v[y] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// np.median + numpyro hpdi(prob 0.68) of the S sorted values
+__device__ void median_hpdi(const double* v, int S, double out3[3]) {
+  out3[0] = (S & 1) ? v[S / 2] : 0.5 * (v[S / 2 - 1] + v[S / 2]);
+  const int len = (int)(0.68 * S);
+  double bw = INFINITY;
+  int best = 0;
+  for (int x = threadIdx.x; x < S - len; x += kWave) {
+    const double w = v[x + len] - v[x];
+    if (w < bw) {  // first minimum per lane
+      bw = w;
+      best = x;
+    }
+  }
+  // wave argmin, ties -> lowest index
+  for (int o = 32; o >= 1; o >>= 1) {
+    const double ow = __shfl_xor(bw, o, 64);
+    const int ob = __shfl_xor(best, o, 64);
+    if (ow < bw || (ow == bw && ob < best)) {
+      bw = ow;
+      best = ob;
+    }
+  }
+  out3[1] = v[best];
+  out3[2] = v[best + len];
+}
+
+__global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __restrict__ gy,
+                                                          const uint32_t* __restrict__ gN,
+                                                          const uint32_t* __restrict__ gmm, int64_t n_taxa,
+                                                          mdfit_opts o, const double* __restrict__ samples,
+                                                          double* __restrict__ out, float* __restrict__ pred,
+                                                          int32_t* __restrict__ status) {
+  __shared__ double s_y[kLD], s_N[kLD];
+  __shared__ uint32_t s_mm[kNPos * kNMM];
+  __shared__ double s_rec[MDFIT_NOUT];
+  __shared__ double s_waic[MDFIT_NSUBFIT][kNPos];
+  __shared__ double s_v[kMaxSamples];
+  const int lane = threadIdx.x;
+  const int64_t t = blockIdx.x;
+  const int S = o.num_samples;
+  if (t >= n_taxa) return;
+  if (lane < kLD) {
+    s_y[lane] = (double)gy[t * kLD + lane];
+    s_N[lane] = (double)gN[t * kLD + lane];
+  }
+  if (gmm != nullptr)
+    for (int x = lane; x < kNPos * kNMM; x += kWave) s_mm[x] = gmm[t * (kNPos * kNMM) + x];
+  for (int x = lane; x < MDFIT_NOUT; x += kWave)
+    s_rec[x] = (x >= MDFIT_NRESULT && x < MDFIT_F_DIAG) ? 0.0 : out[t * MDFIT_NOUT + x];
+  __syncthreads();
+  const bool bad_lane = lane < kNPos && s_y[lane] > s_N[lane];
+  if (__any(bad_lane)) {
+    for (int x = lane; x < MDFIT_NOUT; x += kWave) out[t * MDFIT_NOUT + x] = NAN;
+    if (pred != nullptr)
+      for (int x = lane; x < MDFIT_NPRED * kNPos; x += kWave) pred[t * (MDFIT_NPRED * kNPos) + x] = NAN;
+    if (lane == 0) status[t] = MDFIT_INVALID;
+    return;
+  }
+  int stt = MDFIT_OK;
+  for (int s = 0; s < MDFIT_NSUBFIT; ++s) stt = max(stt, (int)s_rec[MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * s + 6]);
+  const double* smp = samples + t * MDFIT_NSUBFIT * (int64_t)S * 4;
+
+  // ---- posterior means of (q, A, c, phi) per chain -> diag slots 0..3 ---------
+  for (int s = 0; s < MDFIT_NSUBFIT; ++s) {
+    double m[4] = {0, 0, 0, 0};
+    for (int x = lane; x < S; x += kWave)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m[j] += smp[((int64_t)s * S + x) * 4 + j];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m[j] = wsum(m[j]) / S;
+    if (lane == 0)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s_rec[MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * s + j] = m[j];
+  }
+  __syncthreads();
+  if (stt != MDFIT_OK) {
+    for (int x = lane; x < MDFIT_NRESULT; x += kWave) s_rec[x] = NAN;
+    if (pred != nullptr)
+      for (int x = lane; x < MDFIT_NPRED * kNPos; x += kWave) pred[t * (MDFIT_NPRED * kNPos) + x] = NAN;
+    __syncthreads();
+    for (int x = lane; x < MDFIT_NOUT; x += kWave) out[t * MDFIT_NOUT + x] = s_rec[x];
+    if (lane == 0) status[t] = stt;
+    return;
+  }
+
+  // ---- waic_i per chain and point (fits.py:126-172), lanes over draws ----------
+  for (int s = 0; s < MDFIT_NSUBFIT; ++s) {
+    const bool pmd = s == 0 || s == 2 || s == 3;
+    const int lo = (s == 3 || s == 5) ? kNHalf : 0, hi = s < 2 ? kNPos : lo + kNHalf;
+    for (int col = lo; col < hi; ++col) {
+      const double yy = s_y[col], nn = s_N[col];
+      const int k = col < kNHalf ? col : col - kNHalf;
+      const double lc = lg3<false>(nn + 1.0).l - lg3<false>(yy + 1.0).l - lg3<false>(nn - yy + 1.0).l;
+      double mx = -INFINITY, sm = 0.0;
+      for (int x = lane; x < S; x += kWave) {
+        const double* th = smp + ((int64_t)s * S + x) * 4;
+        const double D = d_at(th, pmd, k), phi = th[3];
+        const double a = D * phi, b = (1.0 - D) * phi;
+        const double lp = lc + (lg3<false>(yy + a).l - lg3<false>(a).l) + (lg3<false>(nn - yy + b).l - lg3<false>(b).l) -
+                          (lg3<false>(nn + phi).l - lg3<false>(a + b).l);
+        s_v[x] = lp;
+        mx = fmax(mx, lp);
+        sm += lp;
+      }
+      mx = wmax(mx);
+      const double mean = wsum(sm) / S;
+      double se = 0.0, var = 0.0;
+      for (int x = lane; x < S; x += kWave) {
+        se += exp(s_v[x] - mx);
+        var += (s_v[x] - mean) * (s_v[x] - mean);
+      }
+      se = wsum(se);
+      var = wsum(var) / S;
+      const double lppd = mx + log(se) - log((double)S);
+      if (lane == 0) s_waic[s][col] = -2.0 * (lppd - var);
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  // ---- n_sigma x3, asymmetry (fits.py:194-227): lane = point ------------------
+  {
+    const double v30 = lane < kNPos ? 1.0 : 0.0;
+    const int p = lane < kNPos ? lane : 0;
+    const double dP = s_waic[0][p], dN = s_waic[1][p];
+    const double d = v30 * (dP - dN);
+    const double md = wsum(d) / kNPos;
+    const double var = wsum(v30 * (d - md) * (d - md)) / kNPos;
+    const double ns = (wsum(v30 * dN) - wsum(v30 * dP)) / sqrt(kNPos * var);
+    // forward / reverse: 15 points each
+    const double vf = lane < kNHalf ? 1.0 : 0.0;
+    const int pf = lane < kNHalf ? lane : 0;
+    const double df = vf * (s_waic[2][pf] - s_waic[4][pf]);
+    const double mdf = wsum(df) / kNHalf;
+    const double varf = wsum(vf * (df - mdf) * (df - mdf)) / kNHalf;
+    const double nsf = (wsum(vf * s_waic[4][pf]) - wsum(vf * s_waic[2][pf])) / sqrt(kNHalf * varf);
+    const int pr_ = lane < kNHalf ? kNHalf + lane : kNHalf;
+    const double dr = vf * (s_waic[3][pr_] - s_waic[5][pr_]);
+    const double mdr = wsum(dr) / kNHalf;
+    const double varr = wsum(vf * (dr - mdr) * (dr - mdr)) / kNHalf;
+    const double nsr = (wsum(vf * s_waic[5][pr_]) - wsum(vf * s_waic[3][pr_])) / sqrt(kNHalf * varr);
+    // asymmetry: PMD-all vs concat(PMD-fwd, PMD-rev)
+    const double fr = lane < kNHalf ? s_waic[2][p] : s_waic[3][p];
+    const double dc = v30 * (dP - fr);
+    const double mdc = wsum(dc) / kNPos;
+    const double varc = wsum(v30 * (dc - mdc) * (dc - mdc)) / kNPos;
+    const double asy = (wsum(v30 * fr) - wsum(v30 * dP)) / sqrt(kNPos * varc);
+    if (lane == 0) {
+      s_rec[MDFIT_F_N_SIGMA] = ns;
+      s_rec[MDFIT_F_N_SIGMA_FORWARD] = nsf;
+      s_rec[MDFIT_F_N_SIGMA_REVERSE] = nsr;
+      s_rec[MDFIT_F_ASYMMETRY] = asy;
+    }
+  }
+  // ---- means (fits.py:266-270, 329, 350) ---------------------------------------
+  {
+    double mdm = 0.0;
+    for (int x = lane; x < S; x += kWave) mdm += smp[(int64_t)x * 4 + 1] + smp[(int64_t)x * 4 + 2];
+    mdm = wsum(mdm) / S;
+    if (lane == 0) {
+      s_rec[MDFIT_F_Q_MEAN] = s_rec[MDFIT_F_DIAG + 0];
+      s_rec[MDFIT_F_CONCENTRATION_MEAN] = s_rec[MDFIT_F_DIAG + 3];
+      s_rec[MDFIT_F_D_MAX_MARGINALIZED_MEAN] = mdm;
+      s_rec[MDFIT_F_Q_MEAN_FORWARD] = s_rec[MDFIT_F_DIAG + 2 * MDFIT_DIAG_STRIDE + 0];
+      s_rec[MDFIT_F_Q_MEAN_REVERSE] = s_rec[MDFIT_F_DIAG + 3 * MDFIT_DIAG_STRIDE + 0];
+    }
+  }
+  __syncthreads();
+  // ---- posterior predictive median / HPDI (fits.py:89-120) ---------------------
+  // columns 0..29 of the PMD-all chain, then position 0 of data_forward under the
+  // forward and the reverse PMD chains (the latter is the :343-348 quirk)
+  for (int job = 0; job < kNPos + 2; ++job) {
+    const int s = job < kNPos ? 0 : job - kNPos + 2;
+    const int col = job < kNPos ? job : 0;
+    const int k = col < kNHalf ? col : col - kNHalf;
+    const double nn = s_N[col];
+    double m3[3];
+    if (nn == 0.0) {
+      m3[0] = m3[1] = m3[2] = NAN;
+    } else {
+      const Stream st = make_stream(o.seed, o.index_base + t, s);
+      for (int x = lane; x < S; x += kWave) s_v[x] = predictive_frac(st, x, col, k, nn, smp + ((int64_t)s * S + x) * 4);
+      __syncthreads();
+      lds_sort(s_v, S);
+      median_hpdi(s_v, S, m3);
+      __syncthreads();
+    }
+    if (lane == 0) {
+      if (job < kNPos && pred != nullptr)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) pred[t * (MDFIT_NPRED * kNPos) + q * kNPos + col] = (float)m3[q];
+      if (job == 0) {
+        s_rec[MDFIT_F_D_MAX] = m3[0];
+        s_rec[MDFIT_F_D_MAX_LOWER_HPDI] = m3[1];
+        s_rec[MDFIT_F_D_MAX_UPPER_HPDI] = m3[2];
+      }
+      if (job == kNPos) s_rec[MDFIT_F_D_MAX_FORWARD] = m3[0];
+      if (job == kNPos + 1) s_rec[MDFIT_F_D_MAX_REVERSE] = m3[0];
+    }
+  }
+  __syncthreads();
+  record_sums_noise(lane, s_y, s_N, s_mm, gmm != nullptr, s_rec);
+  __syncthreads();
+  for (int x = lane; x < MDFIT_NOUT; x += kWave) out[t * MDFIT_NOUT + x] = s_rec[x];
+  if (lane == 0) status[t] = stt;
+}
+
+// potential + gradient of item i (model 0 PMD / 1 null, subset 0 all / 1 fwd /
+// 2 rev) at v, by the chain kernel's own layout and code (parity tests)
+__global__ __launch_bounds__(kWave) void nuts_potential_kernel(const int32_t* __restrict__ model,
+                                                               const int32_t* __restrict__ subset,
+                                                               const uint32_t* __restrict__ gy,
+                                                               const uint32_t* __restrict__ gN,
+                                                               const double* __restrict__ gv, int64_t n,
+                                                               double* __restrict__ U, double* __restrict__ g) {
+  const int64_t it = blockIdx.x;
+  if (it >= n) return;
+  const int lane = threadIdx.x, r = lane & 31, h = r >> 4, k = r & 15;
+  const bool whole = subset[it] == 0;
+  PointData pd;
+  pd.pmd = model[it] == 0;
+  pd.valid = (whole ? lane < 32 : lane < 16) && k < kNHalf;
+  pd.k = pd.valid ? k : 0;
+  const int col = pd.valid ? (whole ? h : (subset[it] == 2 ? 1 : 0)) * kNHalf + k : 0;
+  pd.y = pd.valid ? (double)gy[it * kLD + col] : 0.0;
+  pd.N = pd.valid ? (double)gN[it * kLD + col] : 0.0;
+  double v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = gv[it * 4 + j];
+  const Pot P = potential(pd, v, whole);
+  if (lane == 0) {
+    U[it] = P.U;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) g[it * 4 + j] = P.g[j];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host
+// ---------------------------------------------------------------------------
+int potential(const int32_t* model, const int32_t* subset, const uint32_t* y, const uint32_t* N, const double* v,
+              int64_t n, double* U, double* g, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(nuts_potential_kernel, dim3((unsigned)n), dim3(kWave), 0, s, model, subset, y, N, v, n, U, g);
+  return host::check_launch("nuts_potential_kernel");
+}
+
+int64_t workspace_bytes(int64_t n_taxa, int num_samples) {
+  return kSamplesOffset + n_taxa * MDFIT_NSUBFIT * (int64_t)(num_samples > 0 ? num_samples : 0) * 4 * 8;
+}
+
+int fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t n_taxa, const mdfit_opts& o,
+              double* out, float* pred, int32_t* status, void* workspace, hipStream_t s) {
+  if (o.num_samples < 2 || o.num_samples > kMaxSamples)
+    return host::set_err(MDFIT_E_ARG, "num_samples must be in [2, 4096]");
+  if (o.num_warmup < 0) return host::set_err(MDFIT_E_ARG, "num_warmup < 0");
+  int* ws = (int*)workspace;
+  double* samples = (double*)((char*)workspace + kSamplesOffset);
+  // diag slots 4..7 are written by the chains; zero the record first
+  if (hipMemsetAsync(out, 0, (size_t)n_taxa * MDFIT_NOUT * sizeof(double), s) != hipSuccess)
+    return host::check_launch("hipMemsetAsync(out)");
+  const int64_t g = host::fit_grid(nuts_chain_kernel, 4 * n_taxa, 2);
+  hipLaunchKernelGGL(nuts_chain_kernel, dim3((unsigned)g), dim3(kWave), 0, s, y, N, n_taxa, o, out, ws, samples);
+  if (int rc = host::check_launch("nuts_chain_kernel")) return rc;
+  hipLaunchKernelGGL(nuts_post_kernel, dim3((unsigned)n_taxa), dim3(kWave), 0, s, y, N, mm, n_taxa, o, samples, out,
+                     pred, status);
+  return host::check_launch("nuts_post_kernel");
+}
+
+}  // namespace mdfit::nuts

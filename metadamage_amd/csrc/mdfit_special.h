@@ -71,6 +71,8 @@ struct LG3 {
   double q;  // trigamma(x)
 };
 
+// kTri = false: lnGamma and psi only (the sampler needs no Hessian)
+template <bool kTri = true>
 __device__ __forceinline__ LG3 lg3(double x) {
   constexpr double kHalfLog2Pi = 0.91893853320467274178;  // 0.5 ln(2 pi)
   double P = 1.0, dP = 0.0, d2P = 0.0;
@@ -80,7 +82,7 @@ __device__ __forceinline__ LG3 lg3(double x) {
 #pragma unroll
     for (int j = 0; j < 10; ++j) {
       const double t = x + (double)j;
-      d2P = fma(d2P, t, 2.0 * dP);
+      if (kTri) d2P = fma(d2P, t, 2.0 * dP);
       dP = fma(dP, t, P);
       P = P * t;
     }
@@ -106,20 +108,22 @@ __device__ __forceinline__ LG3 lg3(double x) {
   sp = fma(r2, -sp, 1.0 / 12.0);
   double Ps = lx - 0.5 * r - r2 * sp;
   // psi1(xs) ~ r + r2/2 + r^3 (1/6 - r2 (1/30 - ...))
-  double sq = fma(r2, -7.0 / 6.0, 691.0 / 2730.0);
-  sq = fma(r2, -sq, 5.0 / 66.0);
-  sq = fma(r2, -sq, 1.0 / 30.0);
-  sq = fma(r2, -sq, 1.0 / 42.0);
-  sq = fma(r2, -sq, 1.0 / 30.0);
-  sq = fma(r2, -sq, 1.0 / 6.0);
-  double Q = r + 0.5 * r2 + r * r2 * sq;
+  double Q = 0.0;
+  if (kTri) {
+    double sq = fma(r2, -7.0 / 6.0, 691.0 / 2730.0);
+    sq = fma(r2, -sq, 5.0 / 66.0);
+    sq = fma(r2, -sq, 1.0 / 30.0);
+    sq = fma(r2, -sq, 1.0 / 42.0);
+    sq = fma(r2, -sq, 1.0 / 30.0);
+    sq = fma(r2, -sq, 1.0 / 6.0);
+    Q = r + 0.5 * r2 + r * r2 * sq;
+  }
   if (shift) {
     const double iP = rcp(P);
     const double s1 = dP * iP;          // sum 1/(x+j)
-    const double s2 = s1 * s1 - d2P * iP;  // sum 1/(x+j)^2
     L -= flog(P);
     Ps -= s1;
-    Q += s2;
+    if (kTri) Q += s1 * s1 - d2P * iP;  // sum 1/(x+j)^2
   }
   return {L, Ps, Q};
 }

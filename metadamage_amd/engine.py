@@ -35,7 +35,7 @@ class FitBatch:
     out: "object"  # torch.float64 [T, NOUT]
     pred: "object"  # torch.float32 [T, 3, 30]
     status: "object"  # torch.int32 [T]
-    workspace: "object" = None  # torch.uint8 [mdfit_workspace_bytes(T)] (work queues)
+    workspace: "object" = None  # torch.uint8 [mdfit_workspace_bytes(T, opts)] (work queues; NUTS: the draws)
 
 
 def to_device_counts(y, N, mm=None, device="cuda"):
@@ -56,7 +56,7 @@ def to_device_counts(y, N, mm=None, device="cuda"):
     return ty, tN, tm
 
 
-def alloc_outputs(n_taxa: int, device="cuda", with_pred: bool = True) -> FitBatch:
+def alloc_outputs(n_taxa: int, device="cuda", with_pred: bool = True, opts: _lib.MdfitOpts | None = None) -> FitBatch:
     torch = _torch()
     out = torch.empty((n_taxa, _lib.NOUT), dtype=torch.float64, device=device)
     pred = (
@@ -65,13 +65,27 @@ def alloc_outputs(n_taxa: int, device="cuda", with_pred: bool = True) -> FitBatc
         else None
     )
     status = torch.empty((n_taxa,), dtype=torch.int32, device=device)
-    return FitBatch(out, pred, status, alloc_workspace(n_taxa, device))
+    return FitBatch(out, pred, status, alloc_workspace(n_taxa, device, opts))
 
 
-def alloc_workspace(n_taxa: int, device="cuda"):
-    """Device scratch mdfit_fit_batch needs for n_taxa taxa (its work queues)."""
+def workspace_bytes(n_taxa: int, opts: _lib.MdfitOpts | None = None) -> int:
+    lib = _lib.load()
+    return int(lib.mdfit_workspace_bytes(int(n_taxa), ctypes.byref(opts) if opts is not None else None))
+
+
+def alloc_workspace(n_taxa: int, device="cuda", opts: _lib.MdfitOpts | None = None):
+    """Device scratch mdfit_fit_batch needs for n_taxa taxa under opts (work
+    queues; in the sampling mode also every chain's draws)."""
     torch = _torch()
-    return torch.empty((int(_lib.load().mdfit_workspace_bytes(int(n_taxa))),), dtype=torch.uint8, device=device)
+    return torch.empty((workspace_bytes(n_taxa, opts),), dtype=torch.uint8, device=device)
+
+
+def samples_view(res: FitBatch, n_taxa: int, opts: _lib.MdfitOpts):
+    """The sampling mode's draws in the workspace: float64 [T][6][S][4] = (q, A, c, phi)."""
+    torch = _torch()
+    S = int(opts.num_samples)
+    n = n_taxa * 6 * S * 4
+    return res.workspace[_lib.SAMPLES_OFFSET:_lib.SAMPLES_OFFSET + 8 * n].view(torch.float64).view(n_taxa, 6, S, 4)
 
 
 def fit_batch_device(ty, tN, tm=None, opts: _lib.MdfitOpts | None = None, res: FitBatch | None = None,
@@ -86,10 +100,10 @@ def fit_batch_device(ty, tN, tm=None, opts: _lib.MdfitOpts | None = None, res: F
     if tm is not None and not (tm.is_cuda and tm.is_contiguous() and tm.numel() == T * _lib.NPOS * _lib.NMM):
         raise ValueError("mm must be a contiguous cuda tensor of T*30*12 uint32")
     if res is None:
-        res = alloc_outputs(T, device=ty.device)
-    if res.workspace is None or res.workspace.numel() < lib.mdfit_workspace_bytes(T):
-        res.workspace = alloc_workspace(T, ty.device)
+        res = alloc_outputs(T, device=ty.device, opts=opts)
     o = opts if opts is not None else _lib.default_opts()
+    if res.workspace is None or res.workspace.numel() < workspace_bytes(T, o):
+        res.workspace = alloc_workspace(T, ty.device, o)
     _lib.check(
         lib.mdfit_fit_batch(
             ctypes.c_void_p(ty.data_ptr()),
@@ -150,6 +164,25 @@ def peak_probe(n_waves: int, iters: int, stream=None):
     sink = torch.empty(n_waves * 64, dtype=torch.float64, device="cuda")
     _lib.check(lib.mdfit_peak_probe(n_waves, iters, ctypes.c_void_p(sink.data_ptr()), _stream_handle(torch, stream)))
     return sink
+
+
+def nuts_potential(model, subset, y, N, v, device="cuda"):
+    """Sampling-mode potential and gradient per item (mdfit_nuts_potential)."""
+    torch = _torch()
+    lib = _lib.load()
+    n = len(model)
+    tm = torch.as_tensor(np.ascontiguousarray(model, dtype=np.int32), device=device)
+    ts = torch.as_tensor(np.ascontiguousarray(subset, dtype=np.int32), device=device)
+    ty = torch.from_numpy(np.ascontiguousarray(y, dtype=np.uint32).view(np.int32)).to(device)
+    tN = torch.from_numpy(np.ascontiguousarray(N, dtype=np.uint32).view(np.int32)).to(device)
+    tv = torch.as_tensor(np.ascontiguousarray(v, dtype=np.float64), device=device)
+    U = torch.empty(n, dtype=torch.float64, device=device)
+    g = torch.empty((n, 4), dtype=torch.float64, device=device)
+    _lib.check(lib.mdfit_nuts_potential(*(ctypes.c_void_p(t.data_ptr()) for t in (tm, ts, ty, tN, tv)), n,
+                                        ctypes.c_void_p(U.data_ptr()), ctypes.c_void_p(g.data_ptr()),
+                                        _stream_handle(torch)))
+    torch.cuda.synchronize()
+    return U.cpu().numpy(), g.cpu().numpy()
 
 
 def profile_enable(on: bool = True) -> None:

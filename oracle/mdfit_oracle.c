@@ -710,3 +710,6 @@ void oracle_init_u(int model, int subset, const uint32_t* y, const uint32_t* N, 
   int lo = subset == 2 ? NHALF : 0, hi = subset == 1 ? NHALF : NPOS;
   init_u(model, y, N, lo, hi, u4);
 }
+
+/* the sampling mode (MDFIT-NUTS v1) */
+#include "mdfit_nuts.c"
