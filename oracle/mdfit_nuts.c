@@ -870,3 +870,16 @@ int oracle_nuts_chain(int model, int subset, const uint32_t* y, const uint32_t* 
   stats4[3] = cs.acc;
   return cs.status;
 }
+
+/* predictive fractions of the draws th[S][4] at all-position column col
+ * (|z|-1 = k, N = Nn) on stream (seed, g, sub) -- for tests of the median /
+ * HPDI step */
+void oracle_nuts_predictive(uint64_t seed, int64_t g, int sub, int col, int k, double Nn, const double* th, int S,
+                            double* frac, double* med_lo_hi) {
+  nstream ns = nstream_make(seed, g, sub);
+  for (int s = 0; s < S; s++) frac[s] = predictive_frac(&ns, s, col, k, Nn, th + 4 * s, 1);
+  double* v = (double*)malloc(sizeof(double) * (size_t)S);
+  memcpy(v, frac, sizeof(double) * (size_t)S);
+  median_hpdi(v, S, med_lo_hi);
+  free(v);
+}
