@@ -53,7 +53,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--taxa", type=int, default=TAXA_PER_GPU, help="taxa per GPU")
+    ap.add_argument("--taxa", type=int, default=0, help="taxa per GPU (default: 10k MAP / 100k NUTS)")
+    ap.add_argument("--mode", choices=["map", "nuts"], default="map",
+                    help="map: config C2 (the headline); nuts: config C3, the reference's sampler")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     return ap.parse_args()
@@ -94,13 +96,14 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     # ---- synthetic shard, resident in HBM before timing -------------------
-    T = args.taxa
-    b = generate(T, seed=1 + rank)
+    nuts = args.mode == "nuts"
+    T = args.taxa or (100_000 if nuts else TAXA_PER_GPU)
+    b = generate(T, seed=(2 if nuts else 1) + rank)  # C2 seed 1, C3 seed 2
     ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm, device=dev)
     rec = alloc_records(T, dev)
     out, pred, status = packed_views(rec, T)
     res = engine.FitBatch(out, pred, status)
-    opts = _lib.default_opts()
+    opts = _lib.default_opts(mode=_lib.MODE_NUTS if nuts else _lib.MODE_MAP, index_base=rank * T)
     stream = torch.cuda.current_stream(dev)
 
     def step():
@@ -142,7 +145,9 @@ def main():
     group_evals = evals[:, 0] + evals[:, 1] + np.maximum(evals[:, 2], evals[:, 3]) + np.maximum(evals[:, 4], evals[:, 5])
     slot_pe = float(30 * group_evals.sum())
 
-    if rank == 0:
+    if rank == 0 and nuts:
+        print(json.dumps(nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, b)), flush=True)
+    elif rank == 0:
         total = T * world * args.steps
         value = total / elapsed
         k_avg_s = fit_ms_sum / n_calls / 1e3
@@ -211,6 +216,86 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, b):
+    """The JSON line of config C3 (the reference's NUTS, 500 warmup + 1000 draws
+    per sub-fit, 6 sub-fits per taxon)."""
+    from metadamage_amd import _lib
+
+    S, W = 1000, 500
+    k_avg_s = fit_ms_sum / n_calls / 1e3
+    # chain kernel: y,N in; 6 x S draws of 4 doubles + 6 x 4 diagnostics out
+    bytes_per_taxon = 240 + 6 * S * 32 + 6 * 32
+    achieved = bytes_per_taxon * T / k_avg_s / 1e9
+    leap = o[:, _lib.F_DIAG + 5 :: _lib.DIAG_STRIDE][:, :6]  # mean leapfrogs per kept iteration
+    point_evals = float((leap * NPTS).sum() * (W + S))  # (warmup iterations counted at the kept rate)
+    line = {
+        "metric": "TaxID damage fits/sec",
+        "value": round(T * world * args.steps / elapsed, 2),
+        "unit": "fits/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (SURVEY.md §8(d) generator, seed 2+rank)",
+        "config": {
+            "workload": "C3: synthetic TaxIDs x +-15 positions per GPU, full Bayesian fit: NUTS 500 warmup + 1000 "
+            "draws for model_PMD + model_null on all/forward/reverse (6 chains per TaxID), WAIC, predictive "
+            "median/HPDI",
+            "taxa_per_gpu": T,
+            "positions": 30,
+            "parallelism": f"taxon-shard x{world}" + (" + RCCL gather" if world > 1 else ""),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 3),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel": "nuts_chain_kernel",
+            "kernel_ms_avg": round(k_avg_s * 1e3, 3),
+            "bytes_per_taxon": bytes_per_taxon,
+            "call_ms_avg": round(call_ms_sum / n_calls, 3),
+        },
+        "leapfrog_point_evals_per_s": round(point_evals / k_avg_s, 1),
+        "mean_leapfrogs_per_iteration": round(float(leap.mean()), 3),
+        "status_ok_frac": float((st == 0).mean()),
+    }
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_nuts(b, args.cpu_threads)
+    return line
+
+
+def cpu_baseline_nuts(b, threads: int):
+    """The CPU oracle's sampler (oracle/mdfit_nuts.c, C + OpenMP, same
+    algorithm) on the first 64 taxa of the workload."""
+    from oracle.oracle import OracleLib
+
+    lib = OracleLib()
+    nthr = threads if threads > 0 else min(16, os.cpu_count() or 1)
+    n = 64
+    t0 = time.perf_counter()
+    lib.nuts_batch(b.y[:n], b.N[:n], b.mm[:n], threads=nthr)
+    dt = time.perf_counter() - t0
+    n1 = 4
+    t1 = time.perf_counter()
+    lib.nuts_batch(b.y[:n1], b.N[:n1], b.mm[:n1], threads=1)
+    d1 = time.perf_counter() - t1
+    return {
+        "value": round(n / dt, 2),
+        "unit": "fits/s",
+        "cores": nthr,
+        "kind": "port",
+        "sample": f"first {n} taxa of the rank-0 workload on {nthr} OpenMP threads ({dt:.2f} s); "
+        f"1-thread rate on the first {n1}: {n1 / d1:.2f} fits/s",
+        "single_thread_value": round(n1 / d1, 2),
+    }
 
 
 def cpu_baseline(b, threads: int):

@@ -52,6 +52,7 @@ def cli_fit(
     substitution_bases_forward: utils.SubstitutionBases = typer.Option(utils.SubstitutionBases.CT),
     substitution_bases_reverse: utils.SubstitutionBases = typer.Option(utils.SubstitutionBases.GA),
     forced: bool = typer.Option(False, "--forced"),
+    inference: str = typer.Option("nuts", help="nuts: NUTS sampling as the reference; map: MAP fit"),
 ):
     """Fitting Ancient Damage.
 
@@ -71,7 +72,10 @@ def cli_fit(
         "substitution_bases_reverse": substitution_bases_reverse.value,
         "forced": forced,
         "version": "0.0.0",
+        "inference": inference,
     }
+    if inference not in ("nuts", "map"):
+        raise typer.BadParameter("--inference must be nuts or map")
     cfg = utils.Config(**d_cfg)
     cfg.add_filenames(filenames)
     main(filenames, cfg)

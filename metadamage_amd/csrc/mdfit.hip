@@ -735,6 +735,8 @@ void prof_record(int slot, hipStream_t s) {
 }
 }  // namespace
 
+void mdfit::host::prof_mark(int slot, hipStream_t s) { prof_record(slot, s); }
+
 extern "C" {
 
 int mdfit_profile_enable(int on) {

@@ -20,6 +20,10 @@ int set_err(int code, const char* msg);
 // hipGetLastError after a launch -> 0 or the hipError_t (message recorded)
 int check_launch(const char* what);
 
+// optional HIP-event timing (mdfit_profile_enable): slot 1 / 2 bracket the
+// dominant kernel of the call
+void prof_mark(int slot, hipStream_t s);
+
 // persistent grid: no more waves than can be resident at once (so every
 // wave starts immediately and pulls work until its queue is drained), a
 // multiple of the 8 queues

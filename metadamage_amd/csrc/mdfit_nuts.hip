@@ -1028,8 +1028,10 @@ int fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t 
   if (hipMemsetAsync(out, 0, (size_t)n_taxa * MDFIT_NOUT * sizeof(double), s) != hipSuccess)
     return host::check_launch("hipMemsetAsync(out)");
   const int64_t g = host::fit_grid(nuts_chain_kernel, 4 * n_taxa, 2);
+  host::prof_mark(1, s);
   hipLaunchKernelGGL(nuts_chain_kernel, dim3((unsigned)g), dim3(kWave), 0, s, y, N, n_taxa, o, out, ws, samples);
   if (int rc = host::check_launch("nuts_chain_kernel")) return rc;
+  host::prof_mark(2, s);
   hipLaunchKernelGGL(nuts_post_kernel, dim3((unsigned)n_taxa), dim3(kWave), 0, s, y, N, mm, n_taxa, o, samples, out,
                      pred, status);
   return host::check_launch("nuts_post_kernel");

@@ -125,6 +125,9 @@ def fit_packed(p: Packed, opts=None):
     if world == 1:
         return engine.fit_batch(p.y, p.N, p.mm, opts)
     lo, hi = shard_range(p.n_taxa, rank, world)
+    if opts is not None:  # the sampler's streams are keyed by the global taxon index
+        opts = _lib.MdfitOpts.from_buffer_copy(opts)
+        opts.index_base = opts.index_base + lo
     cap = shard_capacity(p.n_taxa, world)
     rec = alloc_records(cap, dev)
     out, pred, status = packed_views(rec, cap)
@@ -173,10 +176,26 @@ def make_df_fit_predictions(p: Packed, pred, keep, cfg) -> pd.DataFrame:
     return utils.downcast_dataframe(df, ["tax_id", "shortname"], fully_automatic=False)
 
 
+def make_opts(cfg, mcmc_kwargs=None):
+    """Engine options for cfg.inference: "nuts" (the reference's sampler,
+    num_warmup / num_samples from mcmc_kwargs as fits.py:792-799 passes them)
+    or "map"."""
+    inference = getattr(cfg, "inference", "nuts")
+    if inference == "map":
+        return _lib.default_opts(mode=_lib.MODE_MAP)
+    if inference != "nuts":
+        raise ValueError(f"inference must be 'nuts' or 'map', got {inference!r}")
+    kw = mcmc_kwargs or {}
+    return _lib.default_opts(mode=_lib.MODE_NUTS, num_warmup=int(kw.get("num_warmup", 500)),
+                             num_samples=int(kw.get("num_samples", 1000)))
+
+
 def compute_fits(df_counts, cfg, mcmc_kwargs=None, opts=None):
     """fits.py:709-730: (df_fit_results, df_fit_predictions) for every taxon of
-    df_counts, in df_counts order.  `mcmc_kwargs` is accepted for signature
-    compatibility; the MAP engine ignores it."""
+    df_counts, in df_counts order, by the sampler (cfg.inference "nuts", the
+    reference's NUTS with mcmc_kwargs' warmup / samples) or the MAP fit."""
+    if opts is None:
+        opts = make_opts(cfg, mcmc_kwargs)
     p = pack_counts(df_counts, cfg)
     res = fit_packed(p, opts)
     if res is None:  # non-zero rank of a multi-GPU job
@@ -202,7 +221,7 @@ def get_top_max_fits(df_counts, N_fits):
 
 
 CACHE_KEYS = ["min_alignments", "min_y_sum", "substitution_bases_forward", "substitution_bases_reverse",
-              "N_fits", "shortname", "filename"]
+              "N_fits", "shortname", "filename", "inference"]
 
 
 def get_fits(df_counts, cfg, opts=None):
@@ -217,7 +236,9 @@ def get_fits(df_counts, cfg, opts=None):
             return parquet_fit_results.load(), parquet_fit_predictions.load()
     logger.info("Fit: Generating fits and saving to file.")
     df_counts_top_N = get_top_max_fits(df_counts, cfg.N_fits)
-    df_fit_results, df_fit_predictions = compute_fits(df_counts_top_N, cfg, opts=opts)
+    # fits.py:792-799
+    mcmc_kwargs = dict(progress_bar=False, num_warmup=500, num_samples=1000, num_chains=1, chain_method="sequential")
+    df_fit_results, df_fit_predictions = compute_fits(df_counts_top_N, cfg, mcmc_kwargs, opts=opts)
     if df_fit_results is None:
         return None, None
     parquet_fit_results.save(df_fit_results, metadata=cfg.to_dict())

@@ -59,6 +59,10 @@ class Config:
 
     N_filenames: Optional[int] = None
     N_fits: Optional[int] = None
+    # this engine's addition: "nuts" samples like the reference (fits.py:382-387),
+    # "map" is the frequentist MAP fit (BASELINE config 2); saved in the parquet
+    # metadata and part of the cache key
+    inference: str = "nuts"
     N_cores: int = field(init=False)
 
     def __post_init__(self):

@@ -49,9 +49,10 @@ def test_parquet_roundtrip_with_metadata(tmp_path, oracle_lib):
     pq.save(dfr, metadata=cfg.to_dict())
     meta = pq.load_metadata()
     assert meta == cfg.to_dict()
+    # the reference's Config keys (utils.py:43-137) + this engine's "inference"
     assert set(meta) == {"out_dir", "max_fits", "max_cores", "min_alignments", "min_y_sum",
                          "substitution_bases_forward", "substitution_bases_reverse", "forced", "version",
-                         "filename", "shortname", "N_filenames", "N_fits", "N_cores"}
+                         "filename", "shortname", "N_filenames", "N_fits", "N_cores", "inference"}
     back = pq.load()
     assert list(back.columns) == list(dfr.columns)
     assert isinstance(back["tax_id"].dtype, pd.CategoricalDtype)

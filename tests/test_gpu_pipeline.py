@@ -27,7 +27,7 @@ def test_cli_fit_fixture_files(tmp_path, oracle_lib, ref_meta):
 
     assert torch.cuda.is_available()
     out_dir = tmp_path / "out"
-    _run(["fit", "--max-fits", "10", "--max-cores", "1", "--out-dir", str(out_dir),
+    _run(["fit", "--max-fits", "10", "--max-cores", "1", "--out-dir", str(out_dir), "--inference", "map",
           str(GOLDEN / "data_ancient.txt"), str(GOLDEN / "data_control.txt")])
     from metadamage_amd import _lib, fits, io, utils
 
@@ -41,7 +41,7 @@ def test_cli_fit_fixture_files(tmp_path, oracle_lib, ref_meta):
         assert res.load_metadata()["N_fits"] == 3 and res.load_metadata()["shortname"] == name
         cfg = utils.Config(out_dir=out_dir, max_fits=10, max_cores=1, min_alignments=10, min_y_sum=10,
                            substitution_bases_forward="CT", substitution_bases_reverse="GA", forced=False,
-                           version="0.0.0")
+                           version="0.0.0", inference="map")
         cfg.add_filename(GOLDEN / f"{name}.txt")
         p = fits.pack_counts(dfc, cfg)
         o, pr, st = oracle_lib.fit_batch(p.y, p.N, p.mm)
@@ -51,9 +51,33 @@ def test_cli_fit_fixture_files(tmp_path, oracle_lib, ref_meta):
         assert len(dfp) == 90
 
 
+def test_cli_default_is_the_reference_sampler(tmp_path, oracle_lib):
+    """Without --inference the fit samples like the reference (NUTS 500 / 1000):
+    same frames; results agree with the oracle's sampler within Monte-Carlo error."""
+    out_dir = tmp_path / "out"
+    _run(["fit", "--out-dir", str(out_dir), str(GOLDEN / "data_ancient.txt")])
+    from metadamage_amd import fits, io, utils
+
+    res = io.Parquet(out_dir / "fit_results" / "data_ancient.parquet")
+    assert res.load_metadata()["inference"] == "nuts"
+    dfr = res.load()
+    dfc = io.Parquet(out_dir / "counts" / "data_ancient.parquet").load()
+    cfg = utils.Config(out_dir=out_dir, max_fits=None, max_cores=1, min_alignments=10, min_y_sum=10,
+                       substitution_bases_forward="CT", substitution_bases_reverse="GA", forced=False,
+                       version="0.0.0")
+    cfg.add_filename(GOLDEN / "data_ancient.txt")
+    p = fits.pack_counts(dfc, cfg)
+    o, pr, st = oracle_lib.nuts_batch(p.y, p.N, p.mm)
+    assert (st == 0).all() and len(dfr) == len(st)
+    # posterior summaries: within a few posterior standard deviations (D_max's HPDI width)
+    width = o[:, 3] - o[:, 2]
+    assert (np.abs(dfr["D_max"].to_numpy() - o[:, 0]) < 0.5 * width + 1e-3).all()
+    np.testing.assert_allclose(dfr["q_mean"].to_numpy(), o[:, 4], rtol=0.2, atol=0.02)
+
+
 def test_cli_cache_and_forced(tmp_path):
     out_dir = tmp_path / "out"
-    args = ["fit", "--out-dir", str(out_dir), str(GOLDEN / "data_ancient.txt")]
+    args = ["fit", "--out-dir", str(out_dir), "--inference", "map", str(GOLDEN / "data_ancient.txt")]
     _run(args)
     f = out_dir / "fit_results" / "data_ancient.parquet"
     m1 = f.stat().st_mtime_ns
