@@ -1,0 +1,359 @@
+// ingest.cpp — memory-mapped, multi-threaded reader of metadamage count
+// tables (include/mdingest.h).
+//
+// mdi_open maps the file, detects the format and cuts it at line boundaries
+// into one chunk per thread, counting each chunk's rows (memchr over
+// newlines).  mdi_parse_into then lets every thread parse its chunk straight
+// into the caller's column arrays at the chunk's row offset -- no growth, no
+// concatenation, no copy -- interning the string columns per chunk (a taxon's
+// rows repeat its name, so the previous row's string is tried first); the
+// chunks' string tables are merged in file order and the codes rewritten in
+// parallel.
+#include "../../include/mdingest.h"
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, long a = 0, long b = 0) {
+  std::snprintf(g_err, sizeof(g_err), fmt, a, b);
+  return code;
+}
+
+struct LocalStrings {
+  std::vector<std::string_view> uniq;
+  std::unordered_map<std::string_view, int32_t> ids;
+  std::string_view last;
+  int32_t last_id = -1;
+  int32_t add(std::string_view s) {
+    if (last_id >= 0 && s == last) return last_id;
+    auto it = ids.find(s);
+    int32_t id;
+    if (it == ids.end()) {
+      id = (int32_t)uniq.size();
+      uniq.push_back(s);
+      ids.emplace(s, id);
+    } else {
+      id = it->second;
+    }
+    last = s;
+    last_id = id;
+    return id;
+  }
+};
+
+struct Chunk {
+  const char* begin = nullptr;
+  const char* end = nullptr;
+  int64_t row0 = 0, rows = 0;  // rows: non-blank lines
+  LocalStrings str[3];
+  int err = 0;
+  long bad_row = 0;
+  int bad_col = 0;
+};
+
+}  // namespace
+
+struct mdi_table {
+  void* map = nullptr;
+  size_t size = 0;
+  const char* data = nullptr;  // first row (after a header)
+  long first_line = 1;
+  int format = 22;
+  int64_t rows = 0;
+  bool parsed = false;
+  std::vector<Chunk> chunks;
+  std::vector<std::string> strings[3];
+};
+
+namespace {
+
+inline bool parse_int(const char*& p, const char* end, int64_t* v) {
+  bool neg = false;
+  if (p < end && (*p == '-' || *p == '+')) {
+    neg = *p == '-';
+    ++p;
+  }
+  const char* s = p;
+  int64_t x = 0;
+  while (p < end && (unsigned)(*p - '0') < 10u) {
+    x = x * 10 + (*p - '0');
+    ++p;
+  }
+  if (p == s) return false;
+  if (p < end && *p == '.') {  // tolerate a float rendering of an integer ("12.0")
+    ++p;
+    while (p < end && *p == '0') ++p;
+    if (p < end && (unsigned)(*p - '0') < 10u) return false;
+  }
+  *v = neg ? -x : x;
+  return true;
+}
+
+inline std::string_view field(const char*& p, const char* end) {
+  const char* s = p;
+  while (p < end && *p != '\t' && *p != '\n' && *p != '\r') ++p;
+  return std::string_view(s, (size_t)(p - s));
+}
+
+inline bool tab(const char*& p, const char* end) {
+  if (p < end && *p == '\t') {
+    ++p;
+    return true;
+  }
+  return false;
+}
+
+inline bool blank_at(const char* p, const char* end) { return p < end && (*p == '\n' || *p == '\r'); }
+
+int64_t count_rows(const char* p, const char* end) {
+  int64_t n = 0;
+  while (p < end) {
+    const char* nl = (const char*)memchr(p, '\n', (size_t)(end - p));
+    const char* le = nl ? nl : end;
+    if (le > p && !(le - p == 1 && *p == '\r')) ++n;  // non-blank line
+    p = nl ? nl + 1 : end;
+  }
+  return n;
+}
+
+struct Out {
+  int64_t *tax_id, *nal, *pos, *counts;
+  int32_t* code[3];
+  int64_t rows;
+};
+
+void parse_chunk(Chunk* c, int format, const Out& o) {
+  const char* p = c->begin;
+  const char* end = c->end;
+  int64_t r = c->row0;
+  const int64_t rend = c->row0 + c->rows;
+  while (p < end) {
+    if (blank_at(p, end)) {
+      ++p;
+      continue;
+    }
+    int col = 0;
+    auto bad = [&](int colno) {
+      c->err = MDI_E_PARSE;
+      c->bad_row = r - c->row0;
+      c->bad_col = colno;
+    };
+    if (r >= rend) return bad(0);  // (rows were counted on the same bytes)
+    int64_t tid, nal, pos;
+    std::string_view name, rank;
+    if (!parse_int(p, end, &tid) || !tab(p, end)) return bad(col);
+    ++col;
+    if (format == 22) {
+      name = field(p, end);
+      if (!tab(p, end)) return bad(col);
+      ++col;
+      rank = field(p, end);
+      if (!tab(p, end)) return bad(col);
+      ++col;
+    }
+    if (!parse_int(p, end, &nal) || !tab(p, end)) return bad(col);
+    ++col;
+    const std::string_view strand = field(p, end);
+    if (!tab(p, end)) return bad(col);
+    ++col;
+    if (!parse_int(p, end, &pos)) return bad(col);
+    ++col;
+    for (int j = 0; j < 16; ++j) {  // column-major: counts[j][rows]
+      int64_t v;
+      if (!tab(p, end) || !parse_int(p, end, &v)) return bad(col);
+      o.counts[(int64_t)j * o.rows + r] = v;
+      ++col;
+    }
+    while (p < end && *p == '\r') ++p;
+    if (p < end && *p != '\n') return bad(col);
+    if (p < end) ++p;
+    o.tax_id[r] = tid;
+    o.nal[r] = nal;
+    o.pos[r] = pos;
+    o.code[MDI_STR_NAME][r] = c->str[MDI_STR_NAME].add(name);
+    o.code[MDI_STR_RANK][r] = c->str[MDI_STR_RANK].add(rank);
+    o.code[MDI_STR_STRAND][r] = c->str[MDI_STR_STRAND].add(strand);
+    ++r;
+  }
+}
+
+template <typename F>
+void parallel_chunks(std::vector<Chunk>& chunks, F f) {
+  std::vector<std::thread> pool;
+  for (size_t i = 1; i < chunks.size(); ++i) pool.emplace_back(f, i);
+  if (!chunks.empty()) f((size_t)0);
+  for (auto& th : pool) th.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+int mdi_open(const char* path, int n_threads, mdi_table** out) {
+  if (!path || !out) return fail(MDI_E_ARG, "null argument");
+  *out = nullptr;
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return fail(MDI_E_IO, "cannot open file");
+  struct stat sb;
+  if (fstat(fd, &sb) != 0) {
+    close(fd);
+    return fail(MDI_E_IO, "cannot stat file");
+  }
+  mdi_table* t = new mdi_table();
+  t->size = (size_t)sb.st_size;
+  if (t->size > 0) {
+    t->map = mmap(nullptr, t->size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+    if (t->map == MAP_FAILED) {
+      close(fd);
+      delete t;
+      return fail(MDI_E_IO, "mmap failed");
+    }
+  }
+  close(fd);
+  const char* base = (const char*)t->map;
+  const char* p = base;
+  const char* end = base + t->size;
+  // format: a '#' header line or 20 tab-separated fields -> the data/input table
+  if (t->size > 0) {
+    const char* eol = (const char*)memchr(p, '\n', t->size);
+    const char* le = eol ? eol : end;
+    int tabs = 0;
+    for (const char* q = p; q < le; ++q) tabs += *q == '\t';
+    if (*p == '#' || tabs + 1 == 20) t->format = 20;
+    if (*p == '#') {
+      p = eol ? eol + 1 : end;
+      t->first_line = 2;
+    }
+  }
+  t->data = p;
+  int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+  if (nt < 1) nt = 1;
+  const size_t span = (size_t)(end - p);
+  if (span < ((size_t)1 << 20)) nt = 1;
+  std::vector<const char*> cuts{p};
+  for (int i = 1; i < nt; ++i) {
+    const char* q = p + span * i / nt;
+    if (q <= cuts.back()) continue;
+    const char* nl = (const char*)memchr(q, '\n', (size_t)(end - q));
+    q = nl ? nl + 1 : end;
+    if (q > cuts.back() && q < end) cuts.push_back(q);
+  }
+  cuts.push_back(end);
+  t->chunks.resize(cuts.size() - 1);
+  for (size_t i = 0; i < t->chunks.size(); ++i) {
+    t->chunks[i].begin = cuts[i];
+    t->chunks[i].end = cuts[i + 1];
+  }
+  parallel_chunks(t->chunks, [&](size_t i) { t->chunks[i].rows = count_rows(t->chunks[i].begin, t->chunks[i].end); });
+  int64_t r = 0;
+  for (Chunk& c : t->chunks) {
+    c.row0 = r;
+    r += c.rows;
+  }
+  t->rows = r;
+  *out = t;
+  g_err[0] = '\0';
+  return 0;
+}
+
+int mdi_format(const mdi_table* t) { return t ? t->format : MDI_E_ARG; }
+int64_t mdi_rows(const mdi_table* t) { return t ? t->rows : MDI_E_ARG; }
+
+int mdi_parse_into(mdi_table* t, int64_t* tax_id, int64_t* n_alignments, int64_t* position, int64_t* counts16,
+                   int32_t* name_code, int32_t* rank_code, int32_t* strand_code) {
+  if (!t || !tax_id || !n_alignments || !position || !counts16 || !name_code || !rank_code || !strand_code)
+    return fail(MDI_E_ARG, "null argument");
+  if (t->parsed) return fail(MDI_E_ARG, "table already parsed");
+  const Out o{tax_id, n_alignments, position, counts16, {name_code, rank_code, strand_code}, t->rows};
+  const int format = t->format;
+  parallel_chunks(t->chunks, [&](size_t i) { parse_chunk(&t->chunks[i], format, o); });
+  for (const Chunk& c : t->chunks)
+    if (c.err) {  // line number of the malformed row: count lines before its chunk
+      long line = t->first_line;
+      for (const char* q = t->data; q < c.begin;) {
+        const char* nl = (const char*)memchr(q, '\n', (size_t)(c.begin - q));
+        if (!nl) break;
+        ++line;
+        q = nl + 1;
+      }
+      return fail(MDI_E_PARSE, "line %ld, column %ld: malformed value", line + c.bad_row, (long)c.bad_col + 1);
+    }
+  // merge the chunks' string tables (file order) and rewrite the codes
+  int32_t* codes[3] = {name_code, rank_code, strand_code};
+  for (int w = 0; w < 3; ++w) {
+    std::unordered_map<std::string_view, int32_t> ids;
+    std::vector<std::vector<int32_t>> remap(t->chunks.size());
+    for (size_t i = 0; i < t->chunks.size(); ++i) {
+      const LocalStrings& ls = t->chunks[i].str[w];
+      remap[i].resize(ls.uniq.size());
+      for (size_t k = 0; k < ls.uniq.size(); ++k) {
+        auto it = ids.find(ls.uniq[k]);
+        if (it == ids.end()) {
+          const int32_t id = (int32_t)t->strings[w].size();
+          t->strings[w].emplace_back(ls.uniq[k]);
+          ids.emplace(ls.uniq[k], id);  // keys view the mapping, alive until mdi_free
+          remap[i][k] = id;
+        } else {
+          remap[i][k] = it->second;
+        }
+      }
+    }
+    parallel_chunks(t->chunks, [&](size_t i) {
+      int32_t* c = codes[w] + t->chunks[i].row0;
+      const std::vector<int32_t>& m = remap[i];
+      for (int64_t k = 0; k < t->chunks[i].rows; ++k) c[k] = m[(size_t)c[k]];
+    });
+  }
+  t->parsed = true;
+  g_err[0] = '\0';
+  return 0;
+}
+
+int64_t mdi_n_strings(const mdi_table* t, int which) {
+  if (!t || which < 0 || which > 2) return MDI_E_ARG;
+  return (int64_t)t->strings[which].size();
+}
+
+int64_t mdi_string_bytes(const mdi_table* t, int which) {
+  if (!t || which < 0 || which > 2) return MDI_E_ARG;
+  int64_t b = 0;
+  for (const std::string& s : t->strings[which]) b += (int64_t)s.size();
+  return b;
+}
+
+int mdi_strings(const mdi_table* t, int which, char* buf, int64_t* offsets) {
+  if (!t || which < 0 || which > 2 || !buf || !offsets) return fail(MDI_E_ARG, "bad arguments");
+  int64_t o = 0;
+  size_t i = 0;
+  for (const std::string& s : t->strings[which]) {
+    offsets[i++] = o;
+    std::memcpy(buf + o, s.data(), s.size());
+    o += (int64_t)s.size();
+  }
+  offsets[i] = o;
+  return 0;
+}
+
+void mdi_free(mdi_table* t) {
+  if (!t) return;
+  if (t->map && t->map != MAP_FAILED) munmap(t->map, t->size);
+  delete t;
+}
+
+const char* mdi_last_error(void) { return g_err; }
+
+}  // extern "C"

@@ -1,0 +1,202 @@
+"""Native count-table reader (libmdingest.so, include/mdingest.h) and the
+vectorised count pipeline on its columns.
+
+The reference reads each input with dask read_csv (counts.py:229-235) and runs
+its per-row pandas pipeline (counts.py:86-209); for a 100k-taxon file (3 M rows,
+~330 MB) that is ~9 s of host time against ~12 ms of GPU fitting.  Here the
+file is memory-mapped and parsed by one thread per chunk, and every pipeline
+step is a numpy expression over the parsed columns; the result is the same
+DataFrame (column order, categories, dtypes) as counts.compute_counts_pandas,
+the line-by-line restatement of the reference.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from pathlib import Path
+
+import numpy as np
+import pandas as pd
+
+LIB_PATH = Path(__file__).resolve().parent / "libmdingest.so"
+_LIB = None
+
+ACTG = "ACGT"
+BASES = [r + o for r in ACTG for o in ACTG]  # AA AC .. TT, the file's column order
+
+
+def _load():
+    global _LIB
+    if _LIB is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"{LIB_PATH} not found: build it (python -c 'import __graft_entry__ as g; g.build()')")
+        lib = ctypes.CDLL(str(LIB_PATH))
+        vp, i64 = ctypes.c_void_p, ctypes.c_int64
+        lib.mdi_open.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(vp)]
+        lib.mdi_open.restype = ctypes.c_int
+        lib.mdi_parse_into.argtypes = [vp] + [vp] * 7
+        lib.mdi_parse_into.restype = ctypes.c_int
+        lib.mdi_format.argtypes = [vp]
+        lib.mdi_format.restype = ctypes.c_int
+        lib.mdi_rows.argtypes = [vp]
+        lib.mdi_rows.restype = i64
+        lib.mdi_n_strings.argtypes = [vp, ctypes.c_int]
+        lib.mdi_n_strings.restype = i64
+        lib.mdi_string_bytes.argtypes = [vp, ctypes.c_int]
+        lib.mdi_string_bytes.restype = i64
+        lib.mdi_strings.argtypes = [vp, ctypes.c_int, vp, vp]
+        lib.mdi_strings.restype = ctypes.c_int
+        lib.mdi_free.argtypes = [vp]
+        lib.mdi_free.restype = None
+        lib.mdi_last_error.restype = ctypes.c_char_p
+        _LIB = lib
+    return _LIB
+
+
+@dataclass
+class Table:
+    format: int  # 22 (reference table) or 20 (data/input table)
+    tax_id: np.ndarray  # int64[rows]
+    n_alignments: np.ndarray
+    position: np.ndarray  # as in the file (0-indexed)
+    counts: np.ndarray  # int64[16][rows], AA .. TT
+    name_code: np.ndarray  # int32[rows] into names
+    names: np.ndarray  # object[n]
+    rank_code: np.ndarray
+    ranks: np.ndarray
+    strand_code: np.ndarray
+    strands: np.ndarray
+
+    @property
+    def rows(self) -> int:
+        return len(self.tax_id)
+
+
+def read_table(path, n_threads: int = 0) -> Table:
+    """Parse a count table with the native reader."""
+    lib = _load()
+    h = ctypes.c_void_p()
+    rc = lib.mdi_open(os.fsencode(str(path)), int(n_threads), ctypes.byref(h))
+    if rc != 0:
+        raise FileNotFoundError(f"{path}: {lib.mdi_last_error().decode()}")
+    try:
+        n = int(lib.mdi_rows(h))
+        cols = [np.empty(n, np.int64) for _ in range(3)]
+        counts = np.empty((16, n), np.int64)  # column-major: one contiguous array per base pair
+        codes = [np.empty(n, np.int32) for _ in range(3)]
+        for a in (*cols, counts, *codes):  # fault the pages in here, not in the parser threads
+            a.fill(0)
+        rc = lib.mdi_parse_into(h, *(c.ctypes.data for c in cols), counts.ctypes.data,
+                                *(c.ctypes.data for c in codes))
+        if rc != 0:
+            raise ValueError(f"{path}: {lib.mdi_last_error().decode()}")
+        tables = []
+        for which in range(3):
+            k = int(lib.mdi_n_strings(h, which))
+            nb = int(lib.mdi_string_bytes(h, which))
+            buf = ctypes.create_string_buffer(max(nb, 1))
+            off = np.empty(k + 1, np.int64)
+            lib.mdi_strings(h, which, buf, off.ctypes.data)
+            raw = buf.raw
+            tables.append(np.array([raw[off[i]:off[i + 1]].decode() for i in range(k)], dtype=object))
+        fmt = int(lib.mdi_format(h))
+    finally:
+        lib.mdi_free(h)
+    return Table(fmt, cols[0], cols[1], cols[2], counts, codes[0], tables[0], codes[1], tables[1], codes[2],
+                 tables[2])
+
+
+def _categorical_from_codes(codes: np.ndarray, table: np.ndarray) -> pd.Categorical:
+    """astype('category') of table[codes] (categories = the sorted distinct
+    values present) without materialising a value per row."""
+    used = np.flatnonzero(np.bincount(codes, minlength=len(table)))
+    vals = table[used]
+    order = np.argsort(vals.astype(str) if vals.dtype == object else vals, kind="stable")
+    remap = np.zeros(len(table), np.int32)
+    remap[used[order]] = np.arange(len(used), dtype=np.int32)
+    return pd.Categorical.from_codes(remap[codes], vals[order])
+
+
+def _row_order(taxon, nal, tax_id, order) -> np.ndarray:
+    """Row permutation of sort_by_alignments (counts.py:167-172): N_alignments,
+    tax_id, order, all descending.  Fast path for the usual layout -- each
+    taxon's rows contiguous, already in order, with one N_alignments -- sorts
+    the taxa only; anything else takes the full three-key sort."""
+    n = len(taxon)
+    if n == 0:
+        return np.zeros(0, np.int64)
+    starts = np.flatnonzero(np.r_[True, taxon[1:] != taxon[:-1]])
+    block = np.repeat(np.arange(len(starts)), np.diff(np.r_[starts, n]))
+    contiguous = len(starts) == len(np.unique(taxon[starts]))
+    if contiguous:
+        same_block = block[1:] == block[:-1]
+        contiguous = bool(np.all(order[1:][same_block] < order[:-1][same_block])) and bool(
+            np.all(nal == nal[starts][block]))
+    if not contiguous:
+        return np.lexsort((-order, -tax_id, -nal))
+    bs = np.lexsort((-tax_id[starts], -nal[starts]))  # blocks: N_alignments, tax_id descending
+    lens = np.diff(np.r_[starts, n])[bs]
+    first = starts[bs]
+    offs = np.repeat(first - np.r_[0, np.cumsum(lens)[:-1]], lens)
+    return np.arange(n) + offs
+
+
+def compute_counts(cfg, table: Table | None = None) -> pd.DataFrame:
+    """counts.py:212-273 on the parsed columns (see counts.compute_counts_pandas
+    for the step-by-step restatement and its reference line numbers)."""
+    t = read_table(cfg.filename) if table is None else table
+    fwd, rev = cfg.substitution_bases_forward, cfg.substitution_bases_reverse
+    col = {b: t.counts[j] for j, b in enumerate(BASES)}
+    # add_reference_counts (counts.py:86-89), in pipeline order
+    extra = {}
+    for ref in (fwd[0], rev[0]):
+        b4 = [b for b in BASES if b[0] == ref]
+        extra[ref] = col[b4[0]] + col[b4[1]] + col[b4[2]] + col[b4[3]]
+    # add_error_rates (counts.py:109-114); fillna(0) turns 0/0 into 0, x/0 stays inf
+    for sub in (fwd, rev):
+        with np.errstate(divide="ignore", invalid="ignore"):
+            f = col[sub] / extra[sub[0]]
+        f[np.isnan(f)] = 0.0
+        extra[f"f_{sub}"] = f
+    # positions: 1-indexed, reverse strand negative (counts.py:117-126)
+    is_fwd = (t.strands == "5'")[t.strand_code]
+    pos = np.where(is_fwd, t.position + 1, -(t.position + 1))
+    # y_sum_total per taxon (counts.py:179-204), then the frozen cut (:207-209)
+    y = np.where(pos > 0, col[fwd], 0) + np.where(pos < 0, col[rev], 0)
+    taxon, uniq = pd.factorize(t.tax_id)
+    ysum = np.zeros(len(uniq), np.int64)
+    np.add.at(ysum, taxon, y)
+    y_sum_total = ysum[taxon]
+    keep = np.flatnonzero((t.n_alignments >= cfg.min_alignments) & (y_sum_total >= cfg.min_y_sum))
+    # sort_by_alignments (counts.py:167-172): N_alignments, tax_id, z = 1..15, -1..-15 (all descending)
+    p = pos[keep]
+    order = np.where(p > 0, 1.0 / np.where(p > 0, p, 1), p)
+    perm = keep[_row_order(taxon[keep], t.n_alignments[keep], t.tax_id[keep], order)]
+
+    tax = taxon[perm]
+    data = {"tax_id": _categorical_from_codes(tax, np.asarray(uniq))}
+    if t.format == 22:
+        data["tax_name"] = _categorical_from_codes(t.name_code[perm], t.names)
+        data["tax_rank"] = _categorical_from_codes(t.rank_code[perm], t.ranks)
+    else:  # the data/input adapter of counts.read_counts_file: "taxid_<id>", "unknown"
+        names = np.array([f"taxid_{v}" for v in uniq], dtype=object)
+        data["tax_name"] = _categorical_from_codes(tax, names)
+        data["tax_rank"] = pd.Categorical.from_codes(np.zeros(len(perm), np.int32), np.array(["unknown"], object))
+    # downcast_dataframe (utils.py:329-356): ints -> uint32 (position int8), floats -> float32
+    ints = [t.n_alignments, *col.values(), *(v for k, v in extra.items() if not k.startswith("f_")), y_sum_total]
+    big = np.iinfo(np.uint32).max
+    if len(perm) and any(int(a.max()) > big for a in ints):  # exact check on the kept rows only if needed
+        if max(int(a[perm].max()) for a in ints) > big:
+            raise AssertionError("Dataframe contains too large values.")
+    data["N_alignments"] = t.n_alignments[perm].astype(np.uint32)
+    data["strand"] = _categorical_from_codes(t.strand_code[perm], t.strands)
+    data["position"] = pos[perm].astype(np.int8)
+    for b in BASES:
+        data[b] = col[b][perm].astype(np.uint32)
+    for k, v in extra.items():
+        data[k] = v[perm].astype(np.float32 if k.startswith("f_") else np.uint32)
+    data["y_sum_total"] = y_sum_total[perm].astype(np.uint32)
+    data["shortname"] = pd.Categorical.from_codes(np.zeros(len(perm), np.int32), np.array([cfg.shortname], object))
+    return pd.DataFrame(data)

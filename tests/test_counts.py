@@ -120,3 +120,70 @@ def test_downcast_raises_on_uint32_overflow():
     df = pd.DataFrame({"a": np.array([2**33], dtype=np.int64)})
     with pytest.raises(AssertionError):
         utils.downcast_dataframe(df, [])
+
+
+# --------------------------------------------------------------------------
+# the native reader (include/mdingest.h) + vectorised pipeline
+# --------------------------------------------------------------------------
+def _cfg(path, fwd="CT", rev="GA", min_alignments=10, min_y_sum=10):
+    cfg = utils.Config(out_dir="/tmp/mdfit_unused", max_fits=None, max_cores=1, min_alignments=min_alignments,
+                       min_y_sum=min_y_sum, substitution_bases_forward=fwd, substitution_bases_reverse=rev,
+                       forced=False, version="0.0.0")
+    cfg.add_filename(path)
+    return cfg
+
+
+@pytest.mark.parametrize("shuffle,bases", [(False, ("CT", "GA")), (True, ("CA", "GT")), (True, ("CT", "CT"))])
+def test_native_pipeline_equals_pandas_restatement(tmp_path, shuffle, bases):
+    """Frame-identical to counts.compute_counts_pandas, on the usual layout (fast
+    row order) and on shuffled rows (full sort), with other substitution bases."""
+    from metadamage_amd import ingest
+    from metadamage_amd.synthetic import generate, to_counts_table
+
+    table = to_counts_table(generate(400, seed=31, fail_fraction=0.2))
+    if shuffle:
+        table = table.sample(frac=1, random_state=1)
+    f = tmp_path / "t.tsv"
+    table.to_csv(f, sep="\t", header=False, index=False)
+    cfg = _cfg(f, *bases)
+    pd.testing.assert_frame_equal(ingest.compute_counts(cfg), counts.compute_counts_pandas(cfg))
+
+
+def test_native_reader_threads_and_line_endings(tmp_path):
+    from metadamage_amd import ingest
+    from metadamage_amd.synthetic import generate, to_counts_table
+
+    table = to_counts_table(generate(3000, seed=32))
+    f = tmp_path / "t.tsv"
+    table.to_csv(f, sep="\t", header=False, index=False)
+    a = ingest.read_table(f, 1)
+    b = ingest.read_table(f, 7)
+    for k in ("tax_id", "n_alignments", "position", "counts", "name_code", "strand_code"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    g = tmp_path / "crlf.tsv"
+    g.write_bytes(f.read_bytes().replace(b"\n", b"\r\n") + b"\r\n")
+    c = ingest.read_table(g, 4)
+    assert np.array_equal(a.counts, c.counts) and list(c.names[c.name_code]) == list(a.names[a.name_code])
+
+
+def test_native_reader_errors(tmp_path):
+    from metadamage_amd import ingest
+
+    with pytest.raises(FileNotFoundError):
+        ingest.read_table(tmp_path / "missing.tsv")
+    f = tmp_path / "bad.tsv"
+    good = "7\tname\tspecies\t100\t5'\t0" + "\t1" * 16 + "\n"
+    f.write_text(good * 3 + "7\tname\tspecies\t100\t5'\tx" + "\t1" * 16 + "\n")
+    with pytest.raises(ValueError, match="line 4, column 6"):
+        ingest.read_table(f)
+
+
+def test_native_reader_on_the_shipped_headed_files():
+    from metadamage_amd import ingest
+
+    for name in ("data_ancient.txt", "data_control.txt"):
+        t = ingest.read_table(GOLDEN / name)
+        raw = pd.read_csv(GOLDEN / name, sep="\t")
+        assert t.format == 20 and t.rows == len(raw)
+        assert np.array_equal(t.tax_id, raw["#taxid"].to_numpy())
+        assert np.array_equal(t.counts.T, raw[[r + o for r in "ACGT" for o in "ACGT"]].to_numpy())
