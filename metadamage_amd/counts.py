@@ -160,9 +160,11 @@ CACHE_KEYS = ["min_alignments", "min_y_sum", "substitution_bases_forward", "subs
               "shortname", "filename"]
 
 
-def load_counts(cfg):
+def load_counts(cfg, writer=None):
     """counts.py:276-306: reuse counts/<shortname>.parquet when its metadata
-    matches on CACHE_KEYS and --forced is off; else compute and save."""
+    matches on CACHE_KEYS and --forced is off; else compute and save (on the
+    `writer` executor when one is given: main() overlaps the write with the
+    next stages)."""
     parquet = io.Parquet(cfg.filename_counts)
     if parquet.exists(cfg.forced):
         if utils.metadata_is_similar(parquet.load_metadata(), cfg.to_dict(), include=CACHE_KEYS):
@@ -172,9 +174,16 @@ def load_counts(cfg):
             return df_counts
     logger.info("Creating DataFrame, please wait.")
     df_counts = compute_counts(cfg)
-    parquet.save(df_counts, metadata=cfg.to_dict())
+    _save(writer, parquet, df_counts, cfg.to_dict())
     cfg.set_number_of_fits(df_counts)
     return df_counts
+
+
+def _save(writer, parquet, df, metadata):
+    if writer is None:
+        parquet.save(df, metadata=metadata)
+    else:
+        writer.submit(parquet.save, df, metadata)
 
 
 def input_is_file(path) -> bool:

@@ -60,6 +60,30 @@ class Packed:
         return len(self.tax_id)
 
 
+def _as_u32(a: np.ndarray) -> np.ndarray:
+    """uint32 view/copy of a count column, with utils.py:338-339's range check."""
+    if a.dtype == np.uint32:
+        return a
+    if a.size and (int(a.max()) > np.iinfo(np.uint32).max or int(a.min()) < 0):
+        raise AssertionError("Dataframe contains too large values.")
+    return a.astype(np.uint32)
+
+
+def _interleave(cols, out2d: np.ndarray, block: int = 16384) -> None:
+    """out2d[:, j] = cols[j], in row blocks that stay cache-resident (a
+    column-at-a-time strided write is ~3x slower on a 2.8 M x 12 table)."""
+    n = out2d.shape[0]
+    for a in range(0, n, block):
+        dst = out2d[a:a + block]
+        for j, c in enumerate(cols):
+            dst[:, j] = c[a:a + block]
+
+
+def _first_values(s: pd.Series, first: np.ndarray) -> np.ndarray:
+    """s.to_numpy()[first] without materialising a categorical column."""
+    return np.asarray(s.array[first]) if isinstance(s.dtype, pd.CategoricalDtype) else s.to_numpy()[first]
+
+
 def pack_counts(df: pd.DataFrame, cfg) -> Packed:
     """Dense y/N (uint32[T][32]) and mismatch counts (uint32[T][30][12]) in
     df order (first appearance of each tax_id, i.e. the N_alignments-desc
@@ -67,38 +91,51 @@ def pack_counts(df: pd.DataFrame, cfg) -> Packed:
     forward substitution, N = its reference-base sum), i >= 15 holds
     z = -(i-14) (reverse substitution) — group_to_numpyro_data, fits.py:398-419.
     Rows are placed by their position value, so missing positions read as
-    N = 0 (no information) instead of shifting the others."""
+    N = 0 (no information) instead of shifting the others.  The usual table
+    (every taxon with its 30 rows in sort_by_alignments order) is packed by
+    reshaping; anything else is scattered row by row."""
     fwd, rev = cfg.substitution_bases_forward, cfg.substitution_bases_reverse
-    tax = df["tax_id"].to_numpy()
-    uniq, first_idx, inv = np.unique(tax, return_index=True, return_inverse=True)
-    order = np.argsort(first_idx, kind="stable")  # taxa in first-appearance order
-    rank = np.empty_like(order)
-    rank[order] = np.arange(order.size)
-    t = rank[inv]
-    T = uniq.size
-    pos = df["position"].to_numpy().astype(np.int64)
-    col = np.where(pos > 0, pos - 1, 14 - pos)
-    ok = (pos != 0) & (np.abs(pos) <= 15)
-    if not ok.all():
-        logger.warning(f"{int((~ok).sum())} rows with |position| outside 1..15 ignored")
-    y = np.zeros((T, _lib.LD), np.uint64)
-    N = np.zeros((T, _lib.LD), np.uint64)
-    yv = np.where(pos > 0, df[fwd].to_numpy(), df[rev].to_numpy()).astype(np.uint64)
-    Nv = np.where(pos > 0, df[fwd[0]].to_numpy(), df[rev[0]].to_numpy()).astype(np.uint64)
-    y[t[ok], col[ok]] = yv[ok]
-    N[t[ok], col[ok]] = Nv[ok]
-    if y.max(initial=0) > np.iinfo(np.uint32).max or N.max(initial=0) > np.iinfo(np.uint32).max:
-        raise AssertionError("Dataframe contains too large values.")  # as utils.py:338-339
-    mm = np.zeros((T, _lib.NPOS, _lib.NMM), np.uint32)
-    mm[t[ok], col[ok], :] = df[MM_COLUMNS].to_numpy()[ok].astype(np.uint32)
-    first = first_idx[order]
+    tax = df["tax_id"]
+    key = tax.cat.codes.to_numpy() if isinstance(tax.dtype, pd.CategoricalDtype) else tax.to_numpy()
+    t, _ = pd.factorize(key)  # taxon index in first-appearance order
+    t = t.astype(np.int64)
+    n = t.size
+    first = np.flatnonzero(np.r_[True, t[1:] > np.maximum.accumulate(t[:-1])]) if n else np.zeros(0, np.int64)
+    T = first.size
+    pos = df["position"].to_numpy()
+    pos_fwd = pos > 0
+    yv = _as_u32(np.where(pos_fwd, df[fwd].to_numpy(), df[rev].to_numpy()))
+    Nv = _as_u32(np.where(pos_fwd, df[fwd[0]].to_numpy(), df[rev[0]].to_numpy()))
+    mm_cols = [_as_u32(df[c].to_numpy()) for c in MM_COLUMNS]
+    dense = n == T * _lib.NPOS and np.array_equal(
+        pos.reshape(T, _lib.NPOS), np.broadcast_to(POSITIONS.astype(pos.dtype), (T, _lib.NPOS))) and np.array_equal(
+        t.reshape(T, _lib.NPOS), np.broadcast_to(np.arange(T)[:, None], (T, _lib.NPOS)))
+    y = np.zeros((T, _lib.LD), np.uint32)
+    N = np.zeros((T, _lib.LD), np.uint32)
+    mm = np.empty((T, _lib.NPOS, _lib.NMM), np.uint32)
+    if dense:
+        y[:, :_lib.NPOS] = yv.reshape(T, _lib.NPOS)
+        N[:, :_lib.NPOS] = Nv.reshape(T, _lib.NPOS)
+        _interleave(mm_cols, mm.reshape(-1, _lib.NMM))
+    else:
+        p64 = pos.astype(np.int64)
+        col = np.where(p64 > 0, p64 - 1, 14 - p64)
+        ok = (p64 != 0) & (np.abs(p64) <= 15)
+        if not ok.all():
+            logger.warning(f"{int((~ok).sum())} rows with |position| outside 1..15 ignored")
+        y[t[ok], col[ok]] = yv[ok]
+        N[t[ok], col[ok]] = Nv[ok]
+        mm.fill(0)
+        rows = np.empty((n, _lib.NMM), np.uint32)
+        _interleave(mm_cols, rows)
+        mm.reshape(-1, _lib.NMM)[(t * _lib.NPOS + col)[ok]] = rows[ok]
     return Packed(
-        tax_id=uniq[order],
-        tax_name=df["tax_name"].to_numpy()[first],
-        tax_rank=df["tax_rank"].to_numpy()[first],
+        tax_id=_first_values(tax, first),
+        tax_name=_first_values(df["tax_name"], first),
+        tax_rank=_first_values(df["tax_rank"], first),
         N_alignments=df["N_alignments"].to_numpy()[first].astype(np.int64),
-        y=y.astype(np.uint32),
-        N=N.astype(np.uint32),
+        y=y,
+        N=N,
         mm=mm,
     )
 
@@ -106,9 +143,10 @@ def pack_counts(df: pd.DataFrame, cfg) -> Packed:
 # --------------------------------------------------------------------------
 # the device call (single GPU or sharded over torch.distributed ranks)
 # --------------------------------------------------------------------------
-def fit_packed(p: Packed, opts=None):
+def fit_packed(p: Packed, opts=None, shard: bool = True):
     """Run mdfit_fit_batch on the packed taxa; returns host (out, pred, status)
-    on rank 0 (None elsewhere in a multi-GPU job)."""
+    on rank 0 (None elsewhere in a multi-GPU job).  shard=False fits every
+    taxon on this rank's GPU (main() shards whole files across ranks)."""
     import torch
 
     from . import engine
@@ -119,7 +157,7 @@ def fit_packed(p: Packed, opts=None):
         raise _lib.MdfitError("metadamage_amd fits run on MI355X GPUs only (no HIP device visible)")
     import torch.distributed as dist
 
-    world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    world = dist.get_world_size() if shard and dist.is_available() and dist.is_initialized() else 1
     rank = dist.get_rank() if world > 1 else 0
     dev = torch.device("cuda", torch.cuda.current_device())
     if world == 1:
@@ -145,35 +183,49 @@ def fit_packed(p: Packed, opts=None):
 # --------------------------------------------------------------------------
 # frames (fits.py:632-680)
 # --------------------------------------------------------------------------
+def _category(values: np.ndarray, repeat: int = 1) -> pd.Categorical:
+    """astype("category") of np.repeat(values, repeat), factorising only the
+    distinct per-taxon values (the frames repeat each taxon 30 times)."""
+    c = pd.Categorical(values)
+    return pd.Categorical.from_codes(np.repeat(c.codes, repeat), c.categories) if repeat != 1 else c
+
+
+def _uint32(v: np.ndarray) -> np.ndarray:
+    if v.size and int(v.max()) > np.iinfo(np.uint32).max:
+        raise AssertionError("Dataframe contains too large values.")  # utils.py:338-339
+    return v.astype(np.uint32)
+
+
 def make_df_fit_results(p: Packed, out, keep, cfg) -> pd.DataFrame:
+    """One row per fitted taxon in FIT_RESULT_COLUMNS order with the dtypes of
+    downcast_dataframe (fits.py:668-680 + utils.py:329-356): names
+    categorical, integer fields uint32, the rest float32."""
     data = {
-        "tax_id": p.tax_id[keep],
-        "tax_name": p.tax_name[keep],
-        "tax_rank": p.tax_rank[keep],
+        "tax_id": _category(p.tax_id[keep]),
+        "tax_name": _category(p.tax_name[keep]),
+        "tax_rank": _category(p.tax_rank[keep]),
     }
     for j, name in enumerate(_lib.RESULT_FIELDS):
         v = out[keep, j]
-        data[name] = np.rint(v).astype(np.int64) if name in INT_RESULT_FIELDS else v
-    data["N_alignments"] = p.N_alignments[keep]
-    df = pd.DataFrame(data)[FIT_RESULT_COLUMNS[:-1]]
-    df["shortname"] = cfg.shortname
-    df = utils.downcast_dataframe(df, ["tax_id", "tax_name", "tax_rank", "shortname"], fully_automatic=False)
-    return df.reset_index(drop=True)
+        data[name] = _uint32(np.rint(v).astype(np.int64)) if name in INT_RESULT_FIELDS else v.astype(np.float32)
+    data["N_alignments"] = _uint32(p.N_alignments[keep])
+    data["shortname"] = pd.Categorical.from_codes(np.zeros(int(keep.sum()), np.int8), [cfg.shortname])
+    return pd.DataFrame({c: data[c] for c in FIT_RESULT_COLUMNS})
 
 
 def make_df_fit_predictions(p: Packed, pred, keep, cfg) -> pd.DataFrame:
+    """fits.py:632-665: 30 rows per fitted taxon (z = 1..15, -1..-15)."""
     n = int(keep.sum())
-    df = pd.DataFrame(
+    return pd.DataFrame(
         {
-            "tax_id": np.repeat(p.tax_id[keep], _lib.NPOS),
-            "position": np.tile(POSITIONS, n),
-            "median": pred[keep, 0, :].reshape(-1).astype(np.float64),
-            "hdpi_lower": pred[keep, 1, :].reshape(-1).astype(np.float64),
-            "hdpi_upper": pred[keep, 2, :].reshape(-1).astype(np.float64),
+            "tax_id": _category(p.tax_id[keep], _lib.NPOS),
+            "position": np.tile(POSITIONS.astype(np.int8), n),
+            "median": pred[keep, 0, :].reshape(-1).astype(np.float32),
+            "hdpi_lower": pred[keep, 1, :].reshape(-1).astype(np.float32),
+            "hdpi_upper": pred[keep, 2, :].reshape(-1).astype(np.float32),
+            "shortname": pd.Categorical.from_codes(np.zeros(n * _lib.NPOS, np.int8), [cfg.shortname]),
         }
     )
-    df["shortname"] = cfg.shortname
-    return utils.downcast_dataframe(df, ["tax_id", "shortname"], fully_automatic=False)
 
 
 def make_opts(cfg, mcmc_kwargs=None):
@@ -190,14 +242,14 @@ def make_opts(cfg, mcmc_kwargs=None):
                              num_samples=int(kw.get("num_samples", 1000)))
 
 
-def compute_fits(df_counts, cfg, mcmc_kwargs=None, opts=None):
+def compute_fits(df_counts, cfg, mcmc_kwargs=None, opts=None, shard=True):
     """fits.py:709-730: (df_fit_results, df_fit_predictions) for every taxon of
     df_counts, in df_counts order, by the sampler (cfg.inference "nuts", the
     reference's NUTS with mcmc_kwargs' warmup / samples) or the MAP fit."""
     if opts is None:
         opts = make_opts(cfg, mcmc_kwargs)
     p = pack_counts(df_counts, cfg)
-    res = fit_packed(p, opts)
+    res = fit_packed(p, opts, shard=shard)
     if res is None:  # non-zero rank of a multi-GPU job
         return None, None
     out, pred, status = res
@@ -224,8 +276,9 @@ CACHE_KEYS = ["min_alignments", "min_y_sum", "substitution_bases_forward", "subs
               "N_fits", "shortname", "filename", "inference"]
 
 
-def get_fits(df_counts, cfg, opts=None):
-    """fits.py:754-807."""
+def get_fits(df_counts, cfg, opts=None, shard=True, writer=None):
+    """fits.py:754-807.  shard: split the taxa over the torch.distributed ranks
+    (rank 0 gathers and saves); writer: an executor for the parquet saves."""
     parquet_fit_results = io.Parquet(cfg.filename_fit_results)
     parquet_fit_predictions = io.Parquet(cfg.filename_fit_predictions)
     if parquet_fit_results.exists(cfg.forced) and parquet_fit_predictions.exists(cfg.forced):
@@ -238,9 +291,11 @@ def get_fits(df_counts, cfg, opts=None):
     df_counts_top_N = get_top_max_fits(df_counts, cfg.N_fits)
     # fits.py:792-799
     mcmc_kwargs = dict(progress_bar=False, num_warmup=500, num_samples=1000, num_chains=1, chain_method="sequential")
-    df_fit_results, df_fit_predictions = compute_fits(df_counts_top_N, cfg, mcmc_kwargs, opts=opts)
+    df_fit_results, df_fit_predictions = compute_fits(df_counts_top_N, cfg, mcmc_kwargs, opts=opts, shard=shard)
     if df_fit_results is None:
         return None, None
-    parquet_fit_results.save(df_fit_results, metadata=cfg.to_dict())
-    parquet_fit_predictions.save(df_fit_predictions, metadata=cfg.to_dict())
+    from .counts import _save
+
+    _save(writer, parquet_fit_results, df_fit_results, cfg.to_dict())
+    _save(writer, parquet_fit_predictions, df_fit_predictions, cfg.to_dict())
     return df_fit_results, df_fit_predictions

@@ -1,34 +1,90 @@
 """Per-file driver (mirror of /root/reference/metadamage/main.py:28-74).
 
 For every input file: validate, load (or compute) the counts table with the
-frozen cuts, then get_fits.  The reference dispatched fits to a process pool
-per file; here get_fits issues one batched GPU call (sharded over ranks when
-torch.distributed is initialised).
+frozen cuts, then get_fits.  The reference ran the files one after another and
+dispatched each file's fits to a process pool; here
+
+  * the stages of consecutive files overlap: a reader thread ingests file
+    i+1 (the native reader releases the GIL) while file i is packed and
+    fitted, and the parquet writes (counts, fit_results, fit_predictions) run
+    on writer threads (pyarrow releases the GIL while encoding);
+  * in a multi-GPU job (torch.distributed initialised) with at least as many
+    files as ranks, whole files are dealt round-robin to the ranks and each
+    rank fits its files on its own GPU -- no collective, nothing replicated;
+    with fewer files than ranks every rank reads every file and the taxa of
+    each are sharded over the ranks (fits.fit_packed, one RCCL gather).
 """
 
 from __future__ import annotations
 
+import copy
 import logging
+from concurrent.futures import ThreadPoolExecutor
 
 from . import counts, fits, utils
 
 logger = logging.getLogger(__name__)
 
+N_WRITERS = 2
+
+
+def _world():
+    try:
+        import torch.distributed as dist
+    except ImportError:  # pragma: no cover
+        return 1, 0
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+class _Writer:
+    """Executor front that remembers its futures so main() can surface a
+    failed write."""
+
+    def __init__(self, pool):
+        self.pool = pool
+        self.futures = []
+
+    def submit(self, fn, *args):
+        self.futures.append(self.pool.submit(fn, *args))
+
+    def drain(self):
+        for f in self.futures:
+            f.result()
+        self.futures.clear()
+
+
+def _load(filename, cfg, writer):
+    cfg_f = copy.copy(cfg)
+    cfg_f.add_filename(filename)
+    return cfg_f, counts.load_counts(cfg_f, writer=writer)
+
 
 def main(filenames, cfg, opts=None):
+    """Fit every file; returns {shortname: (df_fit_results, df_fit_predictions)}
+    for the files this rank fitted (rank 0 holds the gathered frames of
+    taxon-sharded files)."""
     N_files = len(filenames)
-    bad_files = 0
-    results = {}
-    for filename in filenames:
-        if not utils.file_is_valid(filename):
-            bad_files += 1
-            continue
-        cfg.add_filename(filename)
-        df_counts = counts.load_counts(cfg)
-        if not utils.is_df_counts_accepted(df_counts, cfg):
-            continue
-        results[cfg.shortname] = fits.get_fits(df_counts, cfg, opts=opts)
-        logger.debug("End of loop\n")
-    if bad_files == N_files:
+    valid = [f for f in filenames if utils.file_is_valid(f)]
+    if N_files and not valid:
         raise Exception("All files were bad!")
+    world, rank = _world()
+    shard_files = world > 1 and len(valid) >= world
+    mine = valid[rank::world] if shard_files else valid
+    results = {}
+    with ThreadPoolExecutor(1) as reader, ThreadPoolExecutor(N_WRITERS) as pool:
+        writer = _Writer(pool)
+        nxt = reader.submit(_load, mine[0], cfg, writer) if mine else None
+        for i in range(len(mine)):
+            cfg_f, df_counts = nxt.result()
+            nxt = reader.submit(_load, mine[i + 1], cfg, writer) if i + 1 < len(mine) else None
+            cfg.add_filename(cfg_f.filename)  # the caller's cfg follows the files as in the reference
+            cfg.N_tax_ids, cfg.N_fits = getattr(cfg_f, "N_tax_ids", None), cfg_f.N_fits
+            if not utils.is_df_counts_accepted(df_counts, cfg_f):
+                continue
+            results[cfg_f.shortname] = fits.get_fits(df_counts, cfg_f, opts=opts, shard=not shard_files,
+                                                     writer=writer)
+            logger.debug("End of loop\n")
+        writer.drain()
     return results

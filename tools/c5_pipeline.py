@@ -1,0 +1,148 @@
+"""Config C5: streamed counts -> fits over several input files (SURVEY.md
+§8(d): 10 files x 100k TaxIDs in the 22-column format, file i from seed
+100+i, 5 % of the taxa built to fail the cuts).
+
+Two measurements:
+  * --stages: each stage of the per-file driver timed in isolation (count
+    ingest + cut + sort, counts parquet, packing, GPU fit, result frames,
+    result parquets) on the first files;
+  * the end-to-end driver, main.main() -- reader / writer threads overlapped,
+    files dealt to ranks under torchrun -- timed from the first read to the
+    last parquet written (max over ranks), reported as taxa fitted per second.
+
+    python tools/c5_pipeline.py --files 10 --taxa 100000 --inference map
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from multiprocessing import Pool
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def _gen(args):
+    path, taxa, seed = args
+    from metadamage_amd.synthetic import generate, to_counts_table
+
+    if not Path(path).exists():
+        tmp = Path(str(path) + ".tmp")
+        to_counts_table(generate(taxa, seed=seed, fail_fraction=0.05)).to_csv(tmp, sep="\t", header=False,
+                                                                               index=False)
+        tmp.rename(path)
+    return path
+
+
+def _cfg(out_dir, inference):
+    from metadamage_amd import utils
+
+    return utils.Config(out_dir=out_dir, max_fits=None, max_cores=1, min_alignments=10, min_y_sum=10,
+                        substitution_bases_forward="CT", substitution_bases_reverse="GA", forced=True,
+                        version="0.0.0", inference=inference)
+
+
+def stages(files, out_dir, inference):
+    import torch
+
+    from metadamage_amd import counts, fits, io
+
+    for f in files:
+        cfg = _cfg(out_dir, inference)
+        cfg.add_filename(f)
+        t = {"file": f.name}
+        s = time.perf_counter()
+        df = counts.compute_counts(cfg)
+        t["ingest_s"] = time.perf_counter() - s
+        s = time.perf_counter()
+        io.Parquet(cfg.filename_counts).save(df, metadata=cfg.to_dict())
+        t["counts_parquet_s"] = time.perf_counter() - s
+        s = time.perf_counter()
+        p = fits.pack_counts(df, cfg)
+        t["pack_s"] = time.perf_counter() - s
+        s = time.perf_counter()
+        out, pred, st = fits.fit_packed(p, fits.make_opts(cfg), shard=False)
+        torch.cuda.synchronize()
+        t["fit_s"] = time.perf_counter() - s
+        s = time.perf_counter()
+        keep = st == 0
+        dfr = fits.make_df_fit_results(p, out, keep, cfg)
+        dfp = fits.make_df_fit_predictions(p, pred, keep, cfg)
+        t["frames_s"] = time.perf_counter() - s
+        s = time.perf_counter()
+        io.Parquet(cfg.filename_fit_results).save(dfr, metadata=cfg.to_dict())
+        io.Parquet(cfg.filename_fit_predictions).save(dfp, metadata=cfg.to_dict())
+        t["results_parquet_s"] = time.perf_counter() - s
+        t["taxa"] = int(p.n_taxa)
+        print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in t.items()}), flush=True)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--files", type=int, default=10)
+    ap.add_argument("--taxa", type=int, default=100_000)
+    ap.add_argument("--inference", default="map")
+    ap.add_argument("--dir", default="/tmp/mdfit_c5")
+    ap.add_argument("--stages", type=int, default=2, help="files to time stage by stage first (0: none)")
+    ap.add_argument("--gen-procs", type=int, default=8)
+    a = ap.parse_args()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        dist.init_process_group("nccl")
+    d = Path(a.dir)
+    (d / "in").mkdir(parents=True, exist_ok=True)
+    files = [d / "in" / f"c5_{i}.tsv" for i in range(a.files)]
+    s = time.perf_counter()
+    if rank == 0:
+        with Pool(min(a.gen_procs, a.files)) as pool:
+            pool.map(_gen, [(f, a.taxa, 100 + i) for i, f in enumerate(files)])
+        print(json.dumps({"generated_s": round(time.perf_counter() - s, 1),
+                          "bytes": sum(f.stat().st_size for f in files)}), flush=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.init()
+    torch.empty(1, device="cuda")
+    from metadamage_amd import engine
+    from metadamage_amd import main as driver
+    from metadamage_amd.synthetic import generate
+
+    b = generate(64, seed=1)  # load the HIP library and warm the fit path outside the timed region
+    engine.fit_batch(b.y, b.N, b.mm)
+    if rank == 0 and a.stages:
+        stages(files[: a.stages], d / "out_stages", a.inference)
+    cfg = _cfg(d / "out", a.inference)
+    cfg.add_filenames(files)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    s = time.perf_counter()
+    res = driver.main(files, cfg)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - s
+    taxa = sum(len(r[0]) for r in res.values() if r[0] is not None)
+    if world > 1:
+        t = torch.tensor([wall, float(taxa)], dtype=torch.float64, device="cuda")
+        w = t.clone()
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        wall, taxa = float(w[0]), int(t[1])
+    if rank == 0:
+        print(json.dumps({"config": "C5", "inference": a.inference, "files": a.files, "ranks": world,
+                          "taxa_fitted": taxa, "wall_s": round(wall, 3), "taxa_per_s": round(taxa / wall, 1),
+                          "s_per_file": round(wall * world / a.files, 3)}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
