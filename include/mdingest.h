@@ -25,6 +25,7 @@ extern "C" {
 #define MDI_E_IO (-1)     /* open / map failed */
 #define MDI_E_PARSE (-2)  /* malformed row (message names line and column) */
 #define MDI_E_ARG (-3)
+#define MDI_E_RANGE (-4)  /* a kept count above uint32 (utils.py:338-339 "too large values") */
 
 /* string columns, interned: codes index the table's string list (first
  * appearance order) */
@@ -56,6 +57,40 @@ int mdi_strings(const mdi_table* t, int which, char* buf, int64_t* offsets);
 
 void mdi_free(mdi_table* t);
 const char* mdi_last_error(void);
+
+/* ---- the count pipeline on parsed rows (counts.py:86-209) ----------------
+ * Stateless: the arguments are the columns mdi_parse_into filled; the strand
+ * of row r is forward iff code_is_fwd[strand_code[r]] ("5'").  sub_fwd /
+ * sub_rev name the substitutions ("CT", "GA").
+ *
+ * mdi_select replaces add_y_sum_counts + the cut + sort_by_alignments
+ * (counts.py:167-209): taxon[r] = first-appearance index of tax_id[r],
+ * y_sum_total[r] = that taxon's substitution-count sum, and perm[0..n) = the
+ * kept rows (N_alignments >= min_alignments, y_sum_total >= min_y_sum) in
+ * N_alignments, tax_id, z order (all descending, ties in file order).
+ * Returns n (>= 0) or a negative MDI_E_* code.  taxon, y_sum_total and perm
+ * hold `rows` entries. */
+int64_t mdi_select(int64_t rows, const int64_t* tax_id, const int64_t* n_alignments, const int64_t* position,
+                   const int64_t* counts16, const int32_t* strand_code, const uint8_t* code_is_fwd,
+                   int32_t n_codes, const char* sub_fwd, const char* sub_rev, int64_t min_alignments,
+                   int64_t min_y_sum, int32_t* taxon, int64_t* y_sum_total, int64_t* perm);
+
+/* mdi_gather writes the numeric columns of the counts table for the rows
+ * perm[0..n_keep), downcast as utils.py:329-356 (add_reference_counts,
+ * add_error_rates, positions: counts.py:86-126): N_alignments, position
+ * (1-indexed, reverse negative, int8), the 16 pair counts ([16][n_keep]),
+ * the two reference-base sums ([2][n_keep], forward then reverse), the two
+ * error rates f = count / reference (0/0 -> 0, x/0 -> inf; [2][n_keep]) and
+ * y_sum_total.  n_threads <= 0: hardware concurrency.  MDI_E_RANGE if a
+ * kept integer exceeds uint32. */
+int mdi_gather(int64_t rows, const int64_t* perm, int64_t n_keep, const int64_t* n_alignments,
+               const int64_t* position, const int64_t* counts16, const int32_t* strand_code,
+               const uint8_t* code_is_fwd, int32_t n_codes, const char* sub_fwd, const char* sub_rev,
+               const int64_t* y_sum_total, int n_threads, uint32_t* o_nal, int8_t* o_position,
+               uint32_t* o_counts16, uint32_t* o_ref2, float* o_f2, uint32_t* o_y_sum_total);
+
+/* message of the last failed mdi_select / mdi_gather on this thread */
+const char* mdi_counts_error(void);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,223 @@
+// counts.cpp — the count pipeline of the reference's ingest on parsed rows
+// (include/mdingest.h: mdi_select / mdi_gather).
+//
+// Restates /root/reference/metadamage/counts.py:86-209 for the columns
+// mdi_parse_into produced:
+//   add_reference_counts   counts.py:86-89    ref = sum of the 4 pairs starting with the base
+//   add_error_rates        counts.py:109-114  f = count / ref (0/0 -> 0, x/0 -> inf)
+//   positions              counts.py:117-126  1-indexed, reverse strand negative
+//   y_sum_total            counts.py:179-204  per tax_id sum of the substitution counts
+//   cut                    counts.py:207-209  N_alignments >= min_alignments & y_sum_total >= min_y_sum
+//   sort_by_alignments     counts.py:167-172  N_alignments, tax_id, 1/z | z, all descending
+//   downcast               utils.py:329-356   ints -> uint32 (position int8), floats -> float32
+// The vectorised numpy restatement of the same steps (metadamage_amd/ingest.py
+// history, counts.compute_counts_pandas line by line) is the parity check.
+//
+// mdi_select finds the kept rows and their order (one pass, plus a sort of
+// the taxa in the usual layout: each tax_id's rows contiguous and already in
+// z order); mdi_gather writes the output columns of the kept rows in that
+// order, one row range per thread.
+
+#include <stdint.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mdingest.h"
+
+namespace {
+
+struct Rows {
+  int64_t n;
+  const int64_t* tax_id;
+  const int64_t* nal;
+  const int64_t* position;
+  const int64_t* counts;  // [16][n]
+  const int32_t* strand_code;
+  const uint8_t* code_is_fwd;
+  int n_codes;
+  const int64_t* col(int k) const { return counts + (int64_t)k * n; }
+  bool fwd(int64_t r) const {
+    const int32_t c = strand_code[r];
+    return c >= 0 && c < n_codes && code_is_fwd[c];
+  }
+  int64_t pos(int64_t r) const { return fwd(r) ? position[r] + 1 : -(position[r] + 1); }
+};
+
+// "AC" -> column index in AA AC .. TT order; -1 if not a base pair
+int pair_index(const char* s) {
+  static const char kBases[] = "ACGT";
+  if (!s || std::strlen(s) != 2) return -1;
+  const char* a = std::strchr(kBases, s[0]);
+  const char* b = std::strchr(kBases, s[1]);
+  if (!a || !b || !s[0] || !s[1]) return -1;
+  return (int)(a - kBases) * 4 + (int)(b - kBases);
+}
+
+double order_key(int64_t p) { return p > 0 ? 1.0 / (double)p : (double)p; }
+
+thread_local char g_cerr[256] = "";
+
+int arg_error(const char* what) {
+  std::snprintf(g_cerr, sizeof g_cerr, "%s", what);
+  return MDI_E_ARG;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t mdi_select(int64_t rows, const int64_t* tax_id, const int64_t* n_alignments, const int64_t* position,
+                   const int64_t* counts16, const int32_t* strand_code, const uint8_t* code_is_fwd,
+                   int32_t n_codes, const char* sub_fwd, const char* sub_rev, int64_t min_alignments,
+                   int64_t min_y_sum, int32_t* taxon, int64_t* y_sum_total, int64_t* perm) {
+  if (rows < 0 || (rows > 0 && (!tax_id || !n_alignments || !position || !counts16 || !strand_code ||
+                                !taxon || !y_sum_total || !perm)) ||
+      n_codes < 0 || (n_codes > 0 && !code_is_fwd))
+    return arg_error("mdi_select: bad arguments");
+  const int kf = pair_index(sub_fwd), kr = pair_index(sub_rev);
+  if (kf < 0 || kr < 0) return arg_error("mdi_select: substitutions must be base pairs like \"CT\"");
+  const Rows R{rows, tax_id, n_alignments, position, counts16, strand_code, code_is_fwd, n_codes};
+  const int64_t* yf = R.col(kf);
+  const int64_t* yr = R.col(kr);
+
+  // taxon index in first-appearance order (pd.factorize), looked up once per run of equal tax_id
+  std::unordered_map<int64_t, int32_t> index;
+  std::vector<int64_t> ysum;
+  int32_t cur = -1;
+  for (int64_t r = 0; r < rows; ++r) {
+    if (r == 0 || tax_id[r] != tax_id[r - 1]) {
+      auto it = index.emplace(tax_id[r], (int32_t)ysum.size());
+      if (it.second) ysum.push_back(0);
+      cur = it.first->second;
+    }
+    taxon[r] = cur;
+    const int64_t p = R.pos(r);
+    ysum[cur] += p > 0 ? yf[r] : (p < 0 ? yr[r] : 0);
+  }
+  int64_t n_keep = 0;
+  for (int64_t r = 0; r < rows; ++r) {
+    y_sum_total[r] = ysum[taxon[r]];
+    if (n_alignments[r] >= min_alignments && y_sum_total[r] >= min_y_sum) perm[n_keep++] = r;
+  }
+
+  // sort_by_alignments.  Usual layout: every taxon's kept rows one contiguous
+  // run, z order already descending within it, one N_alignments per run ->
+  // sort the runs only.  Otherwise the full three-key sort (stable: ties keep
+  // file order, as np.lexsort).
+  std::vector<int64_t> starts;
+  bool runs_ok = true;
+  {
+    std::vector<uint8_t> seen(ysum.size(), 0);
+    for (int64_t i = 0; i < n_keep && runs_ok; ++i) {
+      const int64_t r = perm[i];
+      if (i == 0 || taxon[r] != taxon[perm[i - 1]]) {
+        if (seen[taxon[r]]) runs_ok = false;
+        seen[taxon[r]] = 1;
+        starts.push_back(i);
+      } else {
+        const int64_t q = perm[i - 1];
+        if (!(order_key(R.pos(r)) < order_key(R.pos(q))) || n_alignments[r] != n_alignments[q]) runs_ok = false;
+      }
+    }
+  }
+  if (runs_ok) {
+    const size_t nb = starts.size();
+    std::vector<int64_t> bs(nb);
+    for (size_t b = 0; b < nb; ++b) bs[b] = (int64_t)b;
+    std::sort(bs.begin(), bs.end(), [&](int64_t a, int64_t b) {
+      const int64_t ra = perm[starts[a]], rb = perm[starts[b]];
+      if (n_alignments[ra] != n_alignments[rb]) return n_alignments[ra] > n_alignments[rb];
+      if (tax_id[ra] != tax_id[rb]) return tax_id[ra] > tax_id[rb];
+      return a < b;
+    });
+    std::vector<int64_t> out((size_t)n_keep);
+    int64_t w = 0;
+    for (size_t k = 0; k < nb; ++k) {
+      const int64_t b = bs[k];
+      const int64_t lo = starts[b], hi = (size_t)b + 1 < nb ? starts[b + 1] : n_keep;
+      for (int64_t i = lo; i < hi; ++i) out[w++] = perm[i];
+    }
+    std::memcpy(perm, out.data(), sizeof(int64_t) * (size_t)n_keep);
+  } else {
+    std::stable_sort(perm, perm + n_keep, [&](int64_t a, int64_t b) {
+      if (n_alignments[a] != n_alignments[b]) return n_alignments[a] > n_alignments[b];
+      if (tax_id[a] != tax_id[b]) return tax_id[a] > tax_id[b];
+      return order_key(R.pos(a)) > order_key(R.pos(b));
+    });
+  }
+  return n_keep;
+}
+
+int mdi_gather(int64_t rows, const int64_t* perm, int64_t n_keep, const int64_t* n_alignments,
+               const int64_t* position, const int64_t* counts16, const int32_t* strand_code,
+               const uint8_t* code_is_fwd, int32_t n_codes, const char* sub_fwd, const char* sub_rev,
+               const int64_t* y_sum_total, int n_threads, uint32_t* o_nal, int8_t* o_position,
+               uint32_t* o_counts16, uint32_t* o_ref2, float* o_f2, uint32_t* o_y_sum_total) {
+  if (n_keep < 0 || (n_keep > 0 && (!perm || !n_alignments || !position || !counts16 || !strand_code ||
+                                    !y_sum_total || !o_nal || !o_position || !o_counts16 || !o_ref2 ||
+                                    !o_f2 || !o_y_sum_total)))
+    return arg_error("mdi_gather: bad arguments");
+  const int kf = pair_index(sub_fwd), kr = pair_index(sub_rev);
+  if (kf < 0 || kr < 0) return arg_error("mdi_gather: substitutions must be base pairs like \"CT\"");
+  const Rows R{rows, nullptr, n_alignments, position, counts16, strand_code, code_is_fwd, n_codes};
+  const int ref_base[2] = {kf / 4, kr / 4};
+  const int sub[2] = {kf, kr};
+  int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+  if (nt < 1) nt = 1;
+  if (n_keep < (int64_t)nt * 65536) nt = (int)std::max<int64_t>(1, n_keep / 65536);
+  if (nt > 64) nt = 64;
+  std::vector<uint8_t> overflow((size_t)nt, 0);  // per thread: a kept value above uint32 (utils.py:338-339)
+  auto work = [&](int tid, int64_t lo, int64_t hi) {
+    const int64_t big = 0xFFFFFFFFll;
+    bool ovf = false;
+    for (int64_t i = lo; i < hi; ++i) {
+      const int64_t r = perm[i];
+      const int64_t nal = n_alignments[r];
+      ovf |= nal > big;
+      o_nal[i] = (uint32_t)nal;
+      o_position[i] = (int8_t)R.pos(r);
+      for (int k = 0; k < 16; ++k) {
+        const int64_t v = R.col(k)[r];
+        ovf |= v > big;
+        o_counts16[(int64_t)k * n_keep + i] = (uint32_t)v;
+      }
+      for (int s = 0; s < 2; ++s) {
+        const int b = ref_base[s];
+        const int64_t ref = R.col(4 * b)[r] + R.col(4 * b + 1)[r] + R.col(4 * b + 2)[r] + R.col(4 * b + 3)[r];
+        ovf |= ref > big;
+        o_ref2[(int64_t)s * n_keep + i] = (uint32_t)ref;
+        const int64_t c = R.col(sub[s])[r];
+        double f;
+        if (ref != 0) f = (double)c / (double)ref;
+        else f = c == 0 ? 0.0 : (c > 0 ? __builtin_inf() : -__builtin_inf());
+        o_f2[(int64_t)s * n_keep + i] = (float)f;
+      }
+      const int64_t ys = y_sum_total[r];
+      ovf |= ys > big;
+      o_y_sum_total[i] = (uint32_t)ys;
+    }
+    overflow[tid] = ovf;
+  };
+  if (nt == 1) {
+    work(0, 0, n_keep);
+  } else {
+    std::vector<std::thread> pool;
+    for (int i = 0; i < nt; ++i) pool.emplace_back(work, i, n_keep * i / nt, n_keep * (i + 1) / nt);
+    for (auto& t : pool) t.join();
+  }
+  for (int i = 0; i < nt; ++i)
+    if (overflow[i]) {
+      std::snprintf(g_cerr, sizeof g_cerr, "Dataframe contains too large values.");
+      return MDI_E_RANGE;
+    }
+  return 0;
+}
+
+const char* mdi_counts_error(void) { return g_cerr; }
+
+}  // extern "C"

@@ -317,7 +317,7 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         t *= 0.5;
         if (t < 1e-12) {
           done = true;
-          status = maxabs4(d) <= 1e-5 ? MDFIT_OK : MDFIT_MAXITER;
+          status = (maxabs4(d) <= 1e-5 || curPg <= kPgTol) ? MDFIT_OK : MDFIT_MAXITER;
         }
       }
       if (!done && evals >= max_iter) {

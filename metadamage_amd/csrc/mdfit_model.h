@@ -26,6 +26,7 @@ __constant__ double kULo[4] = {-25.0, -25.0, 0.0, -25.0};
 __constant__ double kUHi[4] = {25.0, 25.0, 0.999, 20.0};
 constexpr double kEpsAct = 1e-8;
 constexpr double kNoiseF = 1.4e-14;  // objective rounding scale (oracle: NOISE_F)
+constexpr double kPgTol = 1e-6;      // exhausted line search + |proj. grad| below: converged (oracle: PG_TOL)
 
 // ---------------------------------------------------------------------------
 // cross-lane sums inside aligned groups of G lanes (G = 2 ... 64)
@@ -343,9 +344,14 @@ __device__ __forceinline__ void newton_dir(bool pmd, const double u[4], const do
   for (int j = 0; j < 4; ++j) {
     const bool fixed = !pmd && (j == 1 || j == 2);
     const double eps = fmin(kEpsBind[j], w);
-    const bool atlo = u[j] - kULo[j] <= eps, athi = kUHi[j] - u[j] <= eps;
-    // on / next to a box bound and not pulled inward by more than kEpsAct
-    const bool bind = (atlo && g[j] > -kEpsAct) || (athi && g[j] < kEpsAct);
+    const double dlo = u[j] - kULo[j], dhi = kUHi[j] - u[j];
+    const bool atlo = dlo <= eps, athi = dhi <= eps;
+    // on / next to a box bound and not pulled inward by more than kEpsAct --
+    // unless, with positive curvature, its own Newton step g/H stops short of
+    // the bound (an interior optimum just inside it)
+    const double hjj = H[hidx(j, j)];
+    const bool bind = (atlo && g[j] > -kEpsAct && (hjj <= 0.0 || g[j] + kEpsAct > hjj * dlo)) ||
+                      (athi && g[j] < kEpsAct && (hjj <= 0.0 || -g[j] + kEpsAct > hjj * dhi));
     dbind[j] = (bind && !fixed) ? (atlo ? kULo[j] : kUHi[j]) - u[j] : 0.0;
     fr[j] = !(fixed || bind);
   }

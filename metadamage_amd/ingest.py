@@ -51,6 +51,13 @@ def _load():
         lib.mdi_free.argtypes = [vp]
         lib.mdi_free.restype = None
         lib.mdi_last_error.restype = ctypes.c_char_p
+        lib.mdi_select.argtypes = [i64, vp, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_char_p, ctypes.c_char_p,
+                                   i64, i64, vp, vp, vp]
+        lib.mdi_select.restype = i64
+        lib.mdi_gather.argtypes = [i64, vp, i64, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_char_p,
+                                   ctypes.c_char_p, vp, ctypes.c_int, vp, vp, vp, vp, vp, vp]
+        lib.mdi_gather.restype = ctypes.c_int
+        lib.mdi_counts_error.restype = ctypes.c_char_p
         _LIB = lib
     return _LIB
 
@@ -119,6 +126,11 @@ def _categorical_from_codes(codes: np.ndarray, table: np.ndarray) -> pd.Categori
     return pd.Categorical.from_codes(remap[codes], vals[order])
 
 
+def _const_category(value, n: int) -> pd.Categorical:
+    """astype("category") of a column holding one value (no categories when empty)."""
+    return pd.Categorical.from_codes(np.zeros(n, np.int32), np.array([value] if n else [], object))
+
+
 def _row_order(taxon, nal, tax_id, order) -> np.ndarray:
     """Row permutation of sort_by_alignments (counts.py:167-172): N_alignments,
     tax_id, order, all descending.  Fast path for the usual layout -- each
@@ -143,9 +155,71 @@ def _row_order(taxon, nal, tax_id, order) -> np.ndarray:
     return np.arange(n) + offs
 
 
-def compute_counts(cfg, table: Table | None = None) -> pd.DataFrame:
-    """counts.py:212-273 on the parsed columns (see counts.compute_counts_pandas
-    for the step-by-step restatement and its reference line numbers)."""
+def _frame(cols: dict) -> pd.DataFrame:
+    """DataFrame over the given arrays without copying them into a
+    consolidated block."""
+    return pd.DataFrame(cols, copy=False)
+
+
+def compute_counts(cfg, table: Table | None = None, n_threads: int = 0) -> pd.DataFrame:
+    """counts.py:212-273 on the parsed columns: the cut, the sort and every
+    numeric column by the native pipeline (mdi_select / mdi_gather,
+    csrc/counts.cpp); the categoricals from the interned string codes.  Same
+    frame as compute_counts_numpy and counts.compute_counts_pandas."""
+    lib = _load()
+    t = read_table(cfg.filename, n_threads) if table is None else table
+    fwd, rev = cfg.substitution_bases_forward, cfg.substitution_bases_reverse
+    n = t.rows
+    is_fwd = np.ascontiguousarray(t.strands == "5'", dtype=np.uint8)
+    taxon = np.empty(n, np.int32)
+    ysum = np.empty(n, np.int64)
+    perm = np.empty(n, np.int64)
+    common = (t.position.ctypes.data, t.counts.ctypes.data, t.strand_code.ctypes.data, is_fwd.ctypes.data,
+              len(is_fwd), fwd.encode(), rev.encode())
+    k = lib.mdi_select(n, t.tax_id.ctypes.data, t.n_alignments.ctypes.data, *common, int(cfg.min_alignments),
+                       int(cfg.min_y_sum), taxon.ctypes.data, ysum.ctypes.data, perm.ctypes.data)
+    if k < 0:
+        raise ValueError(lib.mdi_counts_error().decode())
+    perm = perm[:k]
+    nal = np.empty(k, np.uint32)
+    pos = np.empty(k, np.int8)
+    c16 = np.empty((16, k), np.uint32)
+    ref2 = np.empty((2, k), np.uint32)
+    f2 = np.empty((2, k), np.float32)
+    ys = np.empty(k, np.uint32)
+    rc = lib.mdi_gather(n, perm.ctypes.data, k, t.n_alignments.ctypes.data, *common, ysum.ctypes.data,
+                        int(n_threads), nal.ctypes.data, pos.ctypes.data, c16.ctypes.data, ref2.ctypes.data,
+                        f2.ctypes.data, ys.ctypes.data)
+    if rc != 0:
+        raise AssertionError(lib.mdi_counts_error().decode())
+    tax = taxon[perm]
+    uniq = t.tax_id[np.flatnonzero(np.r_[True, taxon[1:] > np.maximum.accumulate(taxon[:-1])])] if n else t.tax_id
+    data = {"tax_id": _categorical_from_codes(tax, uniq)}
+    if t.format == 22:
+        data["tax_name"] = _categorical_from_codes(t.name_code[perm], t.names)
+        data["tax_rank"] = _categorical_from_codes(t.rank_code[perm], t.ranks)
+    else:  # the data/input adapter of counts.read_counts_file: "taxid_<id>", "unknown"
+        data["tax_name"] = _categorical_from_codes(tax, np.array([f"taxid_{v}" for v in uniq], dtype=object))
+        data["tax_rank"] = _const_category("unknown", k)
+    data["N_alignments"] = nal
+    data["strand"] = _categorical_from_codes(t.strand_code[perm], t.strands)
+    data["position"] = pos
+    for j, b in enumerate(BASES):
+        data[b] = c16[j]
+    data[fwd[0]] = ref2[0]
+    data[rev[0]] = ref2[1]  # same key as the forward one when both start with one base: the later wins
+    data[f"f_{fwd}"] = f2[0]
+    data[f"f_{rev}"] = f2[1]
+    data["y_sum_total"] = ys
+    data["shortname"] = _const_category(cfg.shortname, k)
+    return _frame(data)
+
+
+def compute_counts_numpy(cfg, table: Table | None = None) -> pd.DataFrame:
+    """counts.py:212-273 as numpy expressions over the parsed columns (the
+    cross-check of compute_counts' native pipeline; see
+    counts.compute_counts_pandas for the step-by-step restatement and its
+    reference line numbers)."""
     t = read_table(cfg.filename) if table is None else table
     fwd, rev = cfg.substitution_bases_forward, cfg.substitution_bases_reverse
     col = {b: t.counts[j] for j, b in enumerate(BASES)}
@@ -183,7 +257,7 @@ def compute_counts(cfg, table: Table | None = None) -> pd.DataFrame:
     else:  # the data/input adapter of counts.read_counts_file: "taxid_<id>", "unknown"
         names = np.array([f"taxid_{v}" for v in uniq], dtype=object)
         data["tax_name"] = _categorical_from_codes(tax, names)
-        data["tax_rank"] = pd.Categorical.from_codes(np.zeros(len(perm), np.int32), np.array(["unknown"], object))
+        data["tax_rank"] = _const_category("unknown", len(perm))
     # downcast_dataframe (utils.py:329-356): ints -> uint32 (position int8), floats -> float32
     ints = [t.n_alignments, *col.values(), *(v for k, v in extra.items() if not k.startswith("f_")), y_sum_total]
     big = np.iinfo(np.uint32).max
@@ -198,5 +272,5 @@ def compute_counts(cfg, table: Table | None = None) -> pd.DataFrame:
     for k, v in extra.items():
         data[k] = v[perm].astype(np.float32 if k.startswith("f_") else np.uint32)
     data["y_sum_total"] = y_sum_total[perm].astype(np.uint32)
-    data["shortname"] = pd.Categorical.from_codes(np.zeros(len(perm), np.int32), np.array([cfg.shortname], object))
+    data["shortname"] = _const_category(cfg.shortname, len(perm))
     return pd.DataFrame(data)

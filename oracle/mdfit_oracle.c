@@ -127,6 +127,8 @@ static const double U_HI[4] = {25.0, 25.0, 0.999, 20.0};
 /* rounding scale of the objective: a trial whose F is within NOISE_F*(sum |lnGamma| + |F|)
  * of the current one is accepted when it lowers the projected gradient */
 #define NOISE_F 1.4e-14
+/* projected-gradient size below which an exhausted line search counts as converged */
+#define PG_TOL 1e-6
 
 static double softplus(double x) { return (x > 0 ? x : 0.0) + log1p(exp(-fabs(x))); }
 static double sigm(double u) { return 1.0 / (1.0 + exp(-u)); }
@@ -315,10 +317,15 @@ static void direction(int model, const double u[4], const double g[4],
   for (int j = 0; j < 4; j++) {
     int fixed = (model == M_NULL && (j == P_A || j == P_C));
     double eps = EPS_BIND[j] < w ? EPS_BIND[j] : w;
-    int atlo = u[j] - U_LO[j] <= eps, athi = U_HI[j] - u[j] <= eps;
+    double dlo = u[j] - U_LO[j], dhi = U_HI[j] - u[j];
+    int atlo = dlo <= eps, athi = dhi <= eps;
     /* a variable on (or next to) its box bound stays there unless the
-     * objective pulls it inward by more than EPS_ACT */
-    int bind = (atlo && g[j] > -EPS_ACT) || (athi && g[j] < EPS_ACT);
+     * objective pulls it inward by more than EPS_ACT -- or, next to the bound
+     * with positive curvature, unless its own Newton step g/H stops short of
+     * the bound (an interior optimum just inside it) */
+    double hjj = H[j][j];
+    int bind = (atlo && g[j] > -EPS_ACT && (hjj <= 0 || g[j] + EPS_ACT > hjj * dlo)) ||
+               (athi && g[j] < EPS_ACT && (hjj <= 0 || -g[j] + EPS_ACT > hjj * dhi));
     if (bind && !fixed) dbind[j] = (atlo ? U_LO[j] : U_HI[j]) - u[j];
     fr[j] = !(fixed || bind);
   }
@@ -443,8 +450,10 @@ static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
       }
     } else {
       t *= 0.5;
-      if (t < 1e-12) { /* line search exhausted: numerically at the optimum */
-        status = (maxabs4(d) <= 1e-5) ? MDFIT_OK : MDFIT_MAXITER;
+      if (t < 1e-12) { /* line search exhausted: numerically at the optimum when
+                          * the step or the projected gradient is negligible (the
+                          * latter: phi creeping to its bound along a flat exp tail) */
+        status = (maxabs4(d) <= 1e-5 || pgnorm(u, cur.g) <= PG_TOL) ? MDFIT_OK : MDFIT_MAXITER;
         break;
       }
     }

@@ -76,3 +76,18 @@ def test_record_layout_constants_match_header():
     enum = re.search(r"enum mdfit_field \{(.*?)MDFIT_NRESULT", text, re.S).group(1)
     fields = re.findall(r"MDFIT_F_([A-Z0-9_]+)", enum)
     assert [f.lower() for f in fields] == [f.lower() for f in _lib.RESULT_FIELDS]
+
+
+def test_ingest_library_exports_every_declared_symbol():
+    """include/mdingest.h (native count reader + pipeline) against libmdingest.so."""
+    from metadamage_amd import ingest
+
+    text = re.sub(r"/\*.*?\*/", "", (ROOT / "include" / "mdingest.h").read_text(), flags=re.S)
+    declared = sorted(set(re.findall(r"\b(mdi_[a-z_0-9]+)\s*\(", text)))
+    assert {"mdi_open", "mdi_parse_into", "mdi_select", "mdi_gather"} <= set(declared)
+    lib = ingest._load()
+    for name in declared:
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", str(ingest.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    assert set(declared) <= set(re.findall(r"\bT (mdi_[a-z_0-9]+)", out))

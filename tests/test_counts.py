@@ -187,3 +187,48 @@ def test_native_reader_on_the_shipped_headed_files():
         assert t.format == 20 and t.rows == len(raw)
         assert np.array_equal(t.tax_id, raw["#taxid"].to_numpy())
         assert np.array_equal(t.counts.T, raw[[r + o for r in "ACGT" for o in "ACGT"]].to_numpy())
+
+
+@pytest.mark.parametrize("layout", ["reversed_within_taxon", "split_runs", "zero_rows", "empty_after_cut"])
+def test_native_pipeline_edge_layouts(tmp_path, layout):
+    """The native select/gather (csrc/counts.cpp) and the numpy restatement
+    agree with the pandas restatement off the usual layout: rows of a taxon out
+    of z order, a taxon's rows in two runs, all-zero rows (0/0 error rates),
+    and a cut that keeps nothing."""
+    from metadamage_amd import ingest
+    from metadamage_amd.synthetic import generate, to_counts_table
+
+    table = to_counts_table(generate(60, seed=33, fail_fraction=0.2))
+    if layout == "reversed_within_taxon":
+        table = table.iloc[::-1]
+    elif layout == "split_runs":
+        table = pd.concat([table.iloc[: len(table) // 2 + 7], table.iloc[len(table) // 2 + 7:]]).iloc[
+            np.r_[np.arange(15), np.arange(len(table) - 20, len(table)), np.arange(15, len(table) - 20)]]
+    elif layout == "zero_rows":
+        table = table.copy()
+        table.iloc[::7, 6:] = 0
+    f = tmp_path / "t.tsv"
+    table.to_csv(f, sep="\t", header=False, index=False)
+    cfg = _cfg(f, min_y_sum=10**12 if layout == "empty_after_cut" else 10)
+    want = counts.compute_counts_pandas(cfg)
+    if layout == "empty_after_cut":
+        assert len(want) == 0
+    pd.testing.assert_frame_equal(ingest.compute_counts(cfg), want)
+    pd.testing.assert_frame_equal(ingest.compute_counts_numpy(cfg), want)
+
+
+def test_native_pipeline_uint32_overflow(tmp_path):
+    """A kept count above uint32 raises as utils.py:338-339; in a row the cut
+    drops it does not."""
+    from metadamage_amd import ingest
+
+    row = lambda tid, nal, pos, big: "\t".join(  # noqa: E731
+        [str(tid), "n", "species", str(nal), "5'", str(pos)] + [str(big)] + ["30"] * 15) + "\n"
+    f = tmp_path / "big.tsv"
+    f.write_text(row(1, 100, 0, 2**32) + row(1, 100, 1, 1))
+    with pytest.raises(AssertionError, match="too large"):
+        ingest.compute_counts(_cfg(f))
+    g = tmp_path / "dropped.tsv"
+    g.write_text(row(1, 100, 0, 5) + row(2, 3, 0, 2**32))  # taxon 2 fails min_alignments
+    df = ingest.compute_counts(_cfg(g))
+    assert list(df["tax_id"].astype(int).unique()) == [1]

@@ -1,0 +1,72 @@
+"""MAP fits whose optimum sits at or just inside a box bound (synthetic C5 /
+C3 taxa that once ended in MDFIT_MAXITER): phi creeping to its lower bound
+along the flat exp tail of u3, and an interior c optimum 6e-5 above c = 0 that
+the old epsilon-active set pinned to the bound.  Both must converge (status
+OK) to a point no feasible nearby point improves on, in the oracle (CPU) and
+in the HIP kernel (GPU, against the oracle)."""
+
+from __future__ import annotations
+
+import json
+
+import numpy as np
+import pytest
+
+from tests.helpers import GOLDEN, RTOL, mixed_rel
+
+CASES = json.loads((GOLDEN / "map_boundary_cases.json").read_text())
+U_LO = np.array([-25.0, -25.0, 0.0, -25.0])
+U_HI = np.array([25.0, 25.0, 0.999, 20.0])
+
+
+def _batch():
+    names = sorted(CASES)
+    y = np.zeros((len(names), 32), np.uint32)
+    N = np.zeros((len(names), 32), np.uint32)
+    for i, n in enumerate(names):
+        y[i, :30] = CASES[n]["y"]
+        N[i, :30] = CASES[n]["N"]
+    return names, y, N
+
+
+def test_oracle_converges_at_bounds(oracle_lib):
+    names, y, N = _batch()
+    out, pred, st = oracle_lib.fit_batch(y, N)
+    assert (st == 0).all(), dict(zip(names, st))
+    assert (out[:, 32 + 6::8][:, :6] == 0).all()  # every sub-fit's own status
+
+
+@pytest.mark.parametrize("subset", [0, 1, 2])
+def test_oracle_subfit_optimum_is_local_min(oracle_lib, subset):
+    """No coordinate step (clamped into the box) lowers F beyond its rounding
+    noise: the returned point is a numerical local minimum."""
+    names, y, N = _batch()
+    rng = np.random.default_rng(subset)
+    for i in range(len(names)):
+        u, F, ev, st = oracle_lib.fit_subfit(0, subset, y[i, :30], N[i, :30])
+        assert st == 0, (names[i], subset)
+        noise = 1e-12 * abs(F) + 1e-9
+        for j in range(4):
+            for h in (1e-4, -1e-4, 1e-6, -1e-6):
+                v = u.copy()
+                v[j] = np.clip(v[j] + h, U_LO[j], U_HI[j])
+                Fv = oracle_lib.objective(0, subset, y[i, :30], N[i, :30], v)[0]
+                assert Fv >= F - noise, (names[i], subset, j, h, F - Fv)
+        for _ in range(8):
+            v = np.clip(u + 1e-5 * rng.standard_normal(4), U_LO, U_HI)
+            assert oracle_lib.objective(0, subset, y[i, :30], N[i, :30], v)[0] >= F - noise
+
+
+@pytest.mark.gpu
+def test_kernel_converges_at_bounds_like_the_oracle(oracle_lib):
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test selected but no HIP device is visible")
+    from metadamage_amd import engine
+
+    names, y, N = _batch()
+    out, pred, st = engine.fit_batch(y, N)
+    ref, rpred, rst = oracle_lib.fit_batch(y, N)
+    assert (st == 0).all() and (rst == 0).all(), (st, rst)
+    assert mixed_rel(out[:, :25], ref[:, :25]).max() < RTOL
