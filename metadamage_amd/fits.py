@@ -46,7 +46,7 @@ INT_RESULT_FIELDS = {"N_alignments", "N_z1_forward", "N_z1_reverse", "N_sum_forw
 # packing: df_counts -> dense [T][32] tensors (batched group_to_numpyro_data)
 # --------------------------------------------------------------------------
 class Packed:
-    def __init__(self, tax_id, tax_name, tax_rank, N_alignments, y, N, mm):
+    def __init__(self, tax_id, tax_name, tax_rank, N_alignments, y, N, mm, cats=None):
         self.tax_id = tax_id
         self.tax_name = tax_name
         self.tax_rank = tax_rank
@@ -54,6 +54,10 @@ class Packed:
         self.y = y
         self.N = N
         self.mm = mm
+        # per-taxon pd.Categorical of tax_id / tax_name / tax_rank when df_counts
+        # had them (sorted categories): the frames reuse their order instead of
+        # re-sorting a million names
+        self.cats = cats or {}
 
     @property
     def n_taxa(self):
@@ -82,6 +86,15 @@ def _interleave(cols, out2d: np.ndarray, block: int = 16384) -> None:
 def _first_values(s: pd.Series, first: np.ndarray) -> np.ndarray:
     """s.to_numpy()[first] without materialising a categorical column."""
     return np.asarray(s.array[first]) if isinstance(s.dtype, pd.CategoricalDtype) else s.to_numpy()[first]
+
+
+def _first_categoricals(df: pd.DataFrame, first: np.ndarray) -> dict:
+    out = {}
+    for c in ("tax_id", "tax_name", "tax_rank"):
+        col = df[c]
+        if isinstance(col.dtype, pd.CategoricalDtype) and col.cat.categories.is_monotonic_increasing:
+            out[c] = col.array[first]
+    return out
 
 
 def pack_counts(df: pd.DataFrame, cfg) -> Packed:
@@ -137,6 +150,7 @@ def pack_counts(df: pd.DataFrame, cfg) -> Packed:
         y=y,
         N=N,
         mm=mm,
+        cats=_first_categoricals(df, first),
     )
 
 
@@ -183,11 +197,19 @@ def fit_packed(p: Packed, opts=None, shard: bool = True):
 # --------------------------------------------------------------------------
 # frames (fits.py:632-680)
 # --------------------------------------------------------------------------
-def _category(values: np.ndarray, repeat: int = 1) -> pd.Categorical:
-    """astype("category") of np.repeat(values, repeat), factorising only the
-    distinct per-taxon values (the frames repeat each taxon 30 times)."""
-    c = pd.Categorical(values)
+def _category(p: Packed, name: str, keep, repeat: int = 1) -> pd.Categorical:
+    """astype("category") of np.repeat(getattr(p, name)[keep], repeat):
+    categories = the sorted distinct values.  From the packed categorical when
+    there is one (its categories are sorted already), else by factorising the
+    per-taxon values once (the predictions repeat each taxon 30 times)."""
+    cat = p.cats.get(name)
+    c = cat[keep].remove_unused_categories() if cat is not None else pd.Categorical(getattr(p, name)[keep])
     return pd.Categorical.from_codes(np.repeat(c.codes, repeat), c.categories) if repeat != 1 else c
+
+
+def _const_category(value, n: int) -> pd.Categorical:
+    """astype("category") of a column holding one value (no categories when empty)."""
+    return pd.Categorical.from_codes(np.zeros(n, np.int8), [value] if n else [])
 
 
 def _uint32(v: np.ndarray) -> np.ndarray:
@@ -201,16 +223,16 @@ def make_df_fit_results(p: Packed, out, keep, cfg) -> pd.DataFrame:
     downcast_dataframe (fits.py:668-680 + utils.py:329-356): names
     categorical, integer fields uint32, the rest float32."""
     data = {
-        "tax_id": _category(p.tax_id[keep]),
-        "tax_name": _category(p.tax_name[keep]),
-        "tax_rank": _category(p.tax_rank[keep]),
+        "tax_id": _category(p, "tax_id", keep),
+        "tax_name": _category(p, "tax_name", keep),
+        "tax_rank": _category(p, "tax_rank", keep),
     }
     for j, name in enumerate(_lib.RESULT_FIELDS):
         v = out[keep, j]
         data[name] = _uint32(np.rint(v).astype(np.int64)) if name in INT_RESULT_FIELDS else v.astype(np.float32)
     data["N_alignments"] = _uint32(p.N_alignments[keep])
-    data["shortname"] = pd.Categorical.from_codes(np.zeros(int(keep.sum()), np.int8), [cfg.shortname])
-    return pd.DataFrame({c: data[c] for c in FIT_RESULT_COLUMNS})
+    data["shortname"] = _const_category(cfg.shortname, int(keep.sum()))
+    return pd.DataFrame({c: data[c] for c in FIT_RESULT_COLUMNS}, copy=False)
 
 
 def make_df_fit_predictions(p: Packed, pred, keep, cfg) -> pd.DataFrame:
@@ -218,13 +240,14 @@ def make_df_fit_predictions(p: Packed, pred, keep, cfg) -> pd.DataFrame:
     n = int(keep.sum())
     return pd.DataFrame(
         {
-            "tax_id": _category(p.tax_id[keep], _lib.NPOS),
+            "tax_id": _category(p, "tax_id", keep, _lib.NPOS),
             "position": np.tile(POSITIONS.astype(np.int8), n),
             "median": pred[keep, 0, :].reshape(-1).astype(np.float32),
             "hdpi_lower": pred[keep, 1, :].reshape(-1).astype(np.float32),
             "hdpi_upper": pred[keep, 2, :].reshape(-1).astype(np.float32),
-            "shortname": pd.Categorical.from_codes(np.zeros(n * _lib.NPOS, np.int8), [cfg.shortname]),
-        }
+            "shortname": _const_category(cfg.shortname, n * _lib.NPOS),
+        },
+        copy=False,
     )
 
 

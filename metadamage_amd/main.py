@@ -25,7 +25,7 @@ from . import counts, fits, utils
 
 logger = logging.getLogger(__name__)
 
-N_WRITERS = 2
+N_WRITERS = 3
 
 
 def _world():
