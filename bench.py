@@ -51,14 +51,19 @@ NPTS = np.array([30, 30, 15, 15, 15, 15])
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None, help="default: 20 (MAP), 1 (NUTS, ~17 s per step)")
+    ap.add_argument("--warmup", type=int, default=None, help="default: 3 (MAP), 1 (NUTS)")
     ap.add_argument("--taxa", type=int, default=0, help="taxa per GPU (default: 10k MAP / 100k NUTS)")
     ap.add_argument("--mode", choices=["map", "nuts"], default="map",
                     help="map: config C2 (the headline); nuts: config C3, the reference's sampler")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.steps is None:
+        a.steps = 20 if a.mode == "map" else 1
+    if a.warmup is None:
+        a.warmup = 3 if a.mode == "map" else 1
+    return a
 
 
 def pmc_traffic():

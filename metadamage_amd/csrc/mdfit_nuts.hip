@@ -254,16 +254,78 @@ struct RowState {
   double wmean[4], wm2[4];     // Welford (slow windows)
 };
 
+// hot per-chain state (row-uniform, in LDS: see nuts_chain_kernel)
+struct ChainState {
+  int mode;
+  bool whole, drained;
+  int64_t taxon;
+  int sub;
+  Stream st;
+  int it, attempt;
+  // dynamics
+  double pz[4], pr[4], pg[4];
+  double step, eps, e0;
+  double invm[4];
+  // step-size search
+  int f_call, f_m, f_last, f_dir;
+  // dual averaging, windows
+  double x_avg, g_avg, mu;
+  int t_da, widx, wn;
+  // tree
+  double t_w, t_rsum[4], t_acc, u_tr;
+  int t_n, t_depth, leaf_ctr, nleap;
+  bool t_turn, t_div, right;
+  // subtree
+  double s_w, s_rsum[4], s_acc;
+  int s_n, n_leaf, nmax;
+  bool s_div;
+  // statistics of the kept iterations
+  double st_div, st_leap;
+};
+
+__device__ __forceinline__ void chain_init(ChainState& c) {
+  c.mode = 0;
+  c.whole = c.drained = false;
+  c.taxon = 0;
+  c.sub = 0;
+  c.st = make_stream(0, 0, 0);
+  c.it = c.attempt = 0;
+  for (int j = 0; j < 4; ++j) {
+    c.pz[j] = c.pr[j] = c.pg[j] = c.t_rsum[j] = c.s_rsum[j] = 0.0;
+    c.invm[j] = 1.0;
+  }
+  c.step = 0.0;
+  c.eps = 1.0;
+  c.e0 = 0.0;
+  c.f_call = c.f_m = c.f_last = c.f_dir = 0;
+  c.x_avg = c.g_avg = c.mu = 0.0;
+  c.t_da = c.widx = c.wn = 0;
+  c.t_w = c.t_acc = c.u_tr = 0.0;
+  c.t_n = c.t_depth = c.leaf_ctr = c.nleap = 0;
+  c.t_turn = c.t_div = false;
+  c.right = true;
+  c.s_w = c.s_acc = 0.0;
+  c.s_n = c.n_leaf = 0;
+  c.nmax = 1;
+  c.s_div = false;
+  c.st_div = c.st_leap = 0.0;
+}
+
 constexpr int kInit = 1, kFind = 2, kIter = 3, kDone = 4;
 
 // ---------------------------------------------------------------------------
 // chain kernel
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kWave) void nuts_chain_kernel(const uint32_t* __restrict__ gy,
+#ifndef MDFIT_NUTS_WAVES_PER_EU
+#define MDFIT_NUTS_WAVES_PER_EU 3  // register budget per lane: 512 / waves (VGPR+AGPR); 3 measured best (C3)
+#endif
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUTS_WAVES_PER_EU))) void nuts_chain_kernel(const uint32_t* __restrict__ gy,
                                                            const uint32_t* __restrict__ gN, int64_t T,
                                                            mdfit_opts o, double* __restrict__ out,
                                                            int* __restrict__ ws, double* __restrict__ samples) {
   __shared__ RowState srow[4];
+  __shared__ ChainState schain[4];
+  __shared__ double sck[8][kWave];  // checkpoint i of a row on its lane i: r[4], rsum[4]
   const int lane = threadIdx.x;
   const int r = lane & 31, h = r >> 4, i = r & 15, row = lane >> 4;
   const int leader = lane & ~31;
@@ -272,6 +334,7 @@ __global__ __launch_bounds__(kWave) void nuts_chain_kernel(const uint32_t* __res
   const int64_t qlo = ntask * qi / kQueues, qhi = ntask * (qi + 1) / kQueues;
   const int W = o.num_warmup, S = o.num_samples;
   RowState& R = srow[row];
+  ChainState& C = schain[row];
 
   PointData pd;
   pd.valid = i < kNHalf;
@@ -279,34 +342,56 @@ __global__ __launch_bounds__(kWave) void nuts_chain_kernel(const uint32_t* __res
   pd.y = pd.N = 0.0;
   pd.pmd = true;
 
-  // task / chain bookkeeping (row-uniform; identical on both rows of a whole chain)
-  int mode = 0;  // 0 idle, kInit, kFind, kIter, kDone
-  bool whole = false, drained = false;
-  int64_t taxon = 0;
-  int sub = 0;
-  Stream st = make_stream(0, 0, 0);
-  int it = 0, attempt = 0;
-  // dynamics
-  double pz[4] = {0, 0, 0, 0}, pr[4] = {0, 0, 0, 0}, pg[4] = {0, 0, 0, 0};
-  double step = 0.0, eps = 1.0, e0 = 0.0;
-  double invm[4] = {1, 1, 1, 1};
-  // step-size search
-  int f_call = 0, f_m = 0, f_last = 0, f_dir = 0;
-  // dual averaging, windows
-  double x_avg = 0.0, g_avg = 0.0, mu = 0.0;
-  int t_da = 0, widx = 0, wn = 0;
-  // tree
-  double t_w = 0.0, t_rsum[4] = {0, 0, 0, 0}, t_acc = 0.0, u_tr = 0.0;
-  int t_n = 0, t_depth = 0, leaf_ctr = 0, nleap = 0;
-  bool t_turn = false, t_div = false, right = true;
-  // subtree
-  double s_w = 0.0, s_rsum[4] = {0, 0, 0, 0}, s_acc = 0.0;
-  int s_n = 0, n_leaf = 0, nmax = 1;
-  bool s_div = false;
-  // checkpoints: lane i < kMaxDepth of the row holds checkpoint i
-  double ck_r[4] = {0, 0, 0, 0}, ck_rs[4] = {0, 0, 0, 0};
-  // statistics of the kept iterations
-  double st_div = 0.0, st_leap = 0.0;
+  // The chain state is row-uniform (every lane of a row holds the same values;
+  // both rows of an all-position chain too) and lives in LDS, so the
+  // potential's registers are what bounds occupancy.
+  int& mode = C.mode;  // 0 idle, kInit, kFind, kIter, kDone
+  bool& whole = C.whole;
+  bool& drained = C.drained;
+  int64_t& taxon = C.taxon;
+  int& sub = C.sub;
+  Stream& st = C.st;
+  int& it = C.it;
+  int& attempt = C.attempt;
+  double* pz = C.pz;
+  double* pr = C.pr;
+  double* pg = C.pg;
+  double& step = C.step;
+  double& eps = C.eps;
+  double& e0 = C.e0;
+  double* invm = C.invm;
+  int& f_call = C.f_call;
+  int& f_m = C.f_m;
+  int& f_last = C.f_last;
+  int& f_dir = C.f_dir;
+  double& x_avg = C.x_avg;
+  double& g_avg = C.g_avg;
+  double& mu = C.mu;
+  int& t_da = C.t_da;
+  int& widx = C.widx;
+  int& wn = C.wn;
+  double& t_w = C.t_w;
+  double* t_rsum = C.t_rsum;
+  double& t_acc = C.t_acc;
+  double& u_tr = C.u_tr;
+  int& t_n = C.t_n;
+  int& t_depth = C.t_depth;
+  int& leaf_ctr = C.leaf_ctr;
+  int& nleap = C.nleap;
+  bool& t_turn = C.t_turn;
+  bool& t_div = C.t_div;
+  bool& right = C.right;
+  double& s_w = C.s_w;
+  double* s_rsum = C.s_rsum;
+  double& s_acc = C.s_acc;
+  int& s_n = C.s_n;
+  int& n_leaf = C.n_leaf;
+  int& nmax = C.nmax;
+  bool& s_div = C.s_div;
+  double& st_div = C.st_div;
+  double& st_leap = C.st_leap;
+  chain_init(C);  // every lane of the row writes the same values
+  for (int j = 0; j < 8; ++j) sck[j][lane] = 0.0;
 
   while (true) {
     // ---- 1. free groups start a task (one atomic per wave-trip) --------------
@@ -377,7 +462,16 @@ __global__ __launch_bounds__(kWave) void nuts_chain_kernel(const uint32_t* __res
       rh[j] = pr[j] - 0.5 * step * pg[j];
       zev[j] = mode == kInit ? pz[j] : pz[j] + step * invm[j] * rh[j];
     }
+#ifdef MDFIT_NUTS_POT_TWICE  // development: marginal cost of one potential evaluation
+    double zev2[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) zev2[j] = zev[j] * (1.0 + 1e-300 * (double)it);
+    const Pot P0 = potential(pd, zev2, whole);
+    Pot P = potential(pd, zev, whole);
+    P.U += 0.0 * P0.U * (double)(it > (1 << 30));
+#else
     const Pot P = potential(pd, zev, whole);
+#endif
     if (!running) continue;
     double rn[4];
 #pragma unroll
@@ -473,15 +567,18 @@ __global__ __launch_bounds__(kWave) void nuts_chain_kernel(const uint32_t* __res
       if ((n_leaf & 1) == 0 && i == imax) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          ck_r[j] = rn[j];
-          ck_rs[j] = s_rsum[j];
+          sck[j][lane] = rn[j];
+          sck[4 + j][lane] = s_rsum[j];
         }
       }
       bool my_turn = false;
       if (i >= imin && i <= imax) {
-        double sub_rsum[4];
+        double ck_r[4], sub_rsum[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) sub_rsum[j] = s_rsum[j] - ck_rs[j] + ck_r[j];
+        for (int j = 0; j < 4; ++j) {
+          ck_r[j] = sck[j][lane];
+          sub_rsum[j] = s_rsum[j] - sck[4 + j][lane] + ck_r[j];
+        }
         my_turn = is_turning(pd.pmd, invm, ck_r, rn, sub_rsum);
       }
       const unsigned long long tm = __ballot(my_turn);

@@ -23,6 +23,8 @@ def main() -> None:
     ap.add_argument("--taxa", type=int, default=10_000)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--mode", choices=["map", "nuts"], default="map")
+    ap.add_argument("--seed", type=int, default=1)
     a = ap.parse_args()
 
     import torch
@@ -30,14 +32,14 @@ def main() -> None:
     from metadamage_amd import _lib, engine
     from metadamage_amd.synthetic import generate
 
-    b = generate(a.taxa, seed=1)
+    b = generate(a.taxa, seed=a.seed)
     ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm)
-    o = _lib.default_opts()
+    o = _lib.default_opts(mode=_lib.MODE_NUTS if a.mode == "nuts" else _lib.MODE_MAP)
     libs = [(p, _lib.load(p)) for p in a.libs]
     ref = None
     for rep in range(a.reps):
         for path, lib in libs:
-            res = engine.alloc_outputs(a.taxa)
+            res = engine.alloc_outputs(a.taxa, opts=o)
 
             def call():
                 _lib.check(lib.mdfit_fit_batch(
@@ -47,7 +49,7 @@ def main() -> None:
                     ctypes.c_void_p(res.status.data_ptr()), ctypes.c_void_p(res.workspace.data_ptr()),
                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
 
-            for _ in range(3):
+            for _ in range(3 if a.mode == "map" else 1):
                 call()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
