@@ -47,6 +47,12 @@ def main() -> None:
             raise SystemExit(f"missing {sub}/*{name} under {src}")
         shutil.copy(cands[0], prof / f"{tag}_{dst}")
         found[dst] = prof / f"{tag}_{dst}"
+    nuts = sorted((src / "nuts_trace").rglob("*kernel_stats.csv"))
+    if nuts:
+        shutil.copy(nuts[0], prof / f"{tag}_nuts_kernel_stats.csv")
+    for name in ("bench_trace.json", "bench_nuts_trace.json"):
+        if (src / name).exists():
+            shutil.copy(src / name, prof / f"{tag}_{name}")
     k = "mdfit::fit_kernel"
     fetch_kb = counter_mean(found["pmc_fetch_size.csv"], k, "FETCH_SIZE")
     write_kb = counter_mean(found["pmc_write_size.csv"], k, "WRITE_SIZE")

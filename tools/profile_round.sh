@@ -2,6 +2,7 @@
 # rocprofv3 passes behind profiles/ (run on the GPU box from the repo root):
 #   bash tools/profile_round.sh r01      (on the box; then locally:
 #   python tools/pmc_summary.py r01 gpurun_out/prof   -> profiles/)
+# plus a kernel-trace pass of the NUTS bench (config C3).
 # kernel trace + stats, then FETCH_SIZE and WRITE_SIZE in separate --pmc passes
 # (never combined with trace domains), then the summary.
 set -o pipefail
@@ -15,4 +16,5 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-for
     python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > /dev/null 2> "$OUT/fetch.err" && \
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- \
     python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > /dev/null 2> "$OUT/write.err" && \
-python3 tools/pmc_summary.py "$TAG" "$OUT"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/nuts_trace" -o run --output-format csv -- \
+    python3 bench.py --mode nuts --no-cpu-baseline > "$OUT/bench_nuts_trace.json" 2> "$OUT/nuts_trace.err"
