@@ -141,7 +141,9 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
   const int leader = lane & ~31;
   const int qi = blockIdx.x % kQueues;
   const int64_t nall = 2 * T;  // all-position tasks: (taxon, model)
-  const int64_t qlo = nall * qi / kQueues, qhi = nall * (qi + 1) / kQueues;
+  // queue qi owns the taxa [tl, tl + nq): first their PMD fits (the long ones,
+  // which also release the long fwd/rev pairs), then their null fits
+  const int64_t tl = T * qi / kQueues, nq = T * (qi + 1) / kQueues - tl;
   int* ring = ws + kWsRing;
 
   // this lane's position: column h*15 + i, |z|-1 = i (lane i = 15 of a half is a pad)
@@ -189,12 +191,12 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       if (lane == 0) base = atomicAdd(ws + qi, __popcll(m));
       base = __shfl(base, 0);
       if (need1) {
-        const int64_t task = qlo + base + __popcll(m & ((1ull << leader) - 1ull));
-        if (task >= qhi) {
+        const int64_t task = (int64_t)base + __popcll(m & ((1ull << leader) - 1ull));
+        if (task >= 2 * nq) {
           all_drained = true;
         } else {
-          sub = task < T ? 0 : 1;  // 0 PMD-all, 1 null-all (task < 2T: no division)
-          taxon = task - (sub ? T : 0);
+          sub = task < nq ? 0 : 1;  // 0 PMD-all, 1 null-all
+          taxon = tl + task - (sub ? nq : 0);
           mode = kAllFit;
           starting = true;
         }

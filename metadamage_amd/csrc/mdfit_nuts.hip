@@ -37,6 +37,23 @@
 
 namespace mdfit::nuts {
 
+#ifdef MDFIT_STAMP
+// diagnostic build (-DMDFIT_STAMP): per-wave cycle split of the chain loop
+// (tools/nuts_stamp_profile.py).  The wave clock (s_memtime) is written to LDS
+// by whichever lanes reach a point; the loop top (converged) books the split of
+// the previous trip.  Never quote this build's run time.
+__device__ unsigned long long* g_nuts_stamp = nullptr;
+__device__ __forceinline__ unsigned long long nstamp() {
+  __builtin_amdgcn_sched_barrier(0);
+  unsigned long long t = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define NSTAMP(k) (sstamp[k] = nstamp())
+#else
+#define NSTAMP(k) ((void)0)
+#endif
+
 constexpr int kMaxDepth = 10;
 constexpr double kMaxDelta = 1000.0;
 constexpr double kTarget = 0.8;
@@ -330,8 +347,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   const int r = lane & 31, h = r >> 4, i = r & 15, row = lane >> 4;
   const int leader = lane & ~31;
   const int qi = blockIdx.x % kQueues;
-  const int64_t ntask = 4 * T;  // [0,2T) all-position chains, [2T,4T) fwd/rev pairs
-  const int64_t qlo = ntask * qi / kQueues, qhi = ntask * (qi + 1) / kQueues;
+  // queue qi owns the taxa [tl, tl + nq) and serves their 4 nq tasks heaviest
+  // kind first: PMD all-position chains, PMD fwd/rev pairs, null all-position,
+  // null pairs (every XCD gets the same mix; long chains start early)
+  const int64_t tl = T * qi / kQueues, nq = T * (qi + 1) / kQueues - tl;
   const int W = o.num_warmup, S = o.num_samples;
   RowState& R = srow[row];
   ChainState& C = schain[row];
@@ -392,8 +411,33 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   double& st_leap = C.st_leap;
   chain_init(C);  // every lane of the row writes the same values
   for (int j = 0; j < 8; ++j) sck[j][lane] = 0.0;
+#ifdef MDFIT_STAMP
+  // [0] top, [1] after the task start, [2] after the potential, [3] after the
+  // mode dispatch, [4] end of the body; acc: start, potential, dispatch, begin, trips
+  __shared__ unsigned long long sstamp[5];
+  unsigned long long acc_t[5] = {0, 0, 0, 0, 0};
+  const unsigned long long t_begin = nstamp();
+  sstamp[0] = 0;
+#endif
 
   while (true) {
+#ifdef MDFIT_STAMP
+    {
+      const unsigned long long now = nstamp();
+      if (sstamp[0] != 0) {  // book the previous trip
+        const unsigned long long t3 = sstamp[3] ? sstamp[3] : now, t4 = sstamp[4] ? sstamp[4] : now;
+        const unsigned long long t2 = sstamp[2] ? sstamp[2] : t3;
+        const unsigned long long t1 = sstamp[1] ? sstamp[1] : t2;
+        acc_t[0] += t1 - sstamp[0];
+        acc_t[1] += t2 - t1;
+        acc_t[2] += t3 - t2;
+        acc_t[3] += now - t3;
+        acc_t[4] += 1;
+      }
+      sstamp[0] = now;
+      sstamp[1] = sstamp[2] = sstamp[3] = sstamp[4] = 0;
+    }
+#endif
     // ---- 1. free groups start a task (one atomic per wave-trip) --------------
     const unsigned long long busy_m = __ballot(mode != 0 && mode != kDone);
     const bool group_free = ((busy_m >> leader) & 0xFFFFFFFFull) == 0ull;
@@ -406,21 +450,15 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       if (lane == 0) base = atomicAdd(ws + qi, __popcll(m));
       base = __shfl(base, 0);
       if (need) {
-        const int64_t task = qlo + base + __popcll(m & ((1ull << leader) - 1ull));
-        if (task >= qhi) {
+        const int64_t task = (int64_t)base + __popcll(m & ((1ull << leader) - 1ull));
+        if (task >= 4 * nq) {
           drained = true;
           mode = 0;
         } else {
-          whole = task < 2 * T;
-          if (whole) {
-            sub = task < T ? 0 : 1;
-            taxon = task - (sub ? T : 0);
-          } else {
-            const int64_t pt = task - 2 * T;
-            const bool pmdm = pt < T;
-            taxon = pmdm ? pt : pt - T;
-            sub = (pmdm ? 2 : 4) + h;
-          }
+          const int kind = (int)(task / nq);
+          taxon = tl + task % nq;
+          whole = kind == 0 || kind == 2;
+          sub = kind == 0 ? 0 : (kind == 2 ? 1 : (kind == 1 ? 2 : 4) + h);
           starting = true;
         }
       }
@@ -452,6 +490,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       }
     }
     if (!__any(mode != 0 || !drained)) break;
+    NSTAMP(1);
     const bool running = mode == kInit || mode == kFind || mode == kIter;
     if (!__any(running)) continue;  // (only finished chains of unfinished groups)
 
@@ -472,6 +511,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
 #else
     const Pot P = potential(pd, zev, whole);
 #endif
+    NSTAMP(2);
     if (!running) continue;
     double rn[4];
 #pragma unroll
@@ -700,6 +740,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       }
     }
 
+    NSTAMP(3);
     if (begin_find) {
       // one probe of find_reasonable_step_size from the current state
       if (mode != kFind || f_m == 0) {
@@ -745,7 +786,15 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       nmax = 1;
       step = right ? eps : -eps;
     }
+    NSTAMP(4);
   }
+#ifdef MDFIT_STAMP
+  if (lane == 0 && g_nuts_stamp) {
+    unsigned long long* w = g_nuts_stamp + 8 * (size_t)blockIdx.x;
+    for (int j = 0; j < 5; ++j) w[j] = acc_t[j];
+    w[5] = nstamp() - t_begin;
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1135,3 +1184,10 @@ int fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t 
 }
 
 }  // namespace mdfit::nuts
+
+#ifdef MDFIT_STAMP
+extern "C" int mdfit_nuts_set_stamp(unsigned long long* buf) {
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(mdfit::nuts::g_nuts_stamp), &buf, sizeof(buf));
+  return 0;
+}
+#endif
