@@ -115,6 +115,15 @@ __device__ __forceinline__ double sel4(const double v[4], int j) {
 
 __device__ __forceinline__ bool active(bool pmd, int j) { return pmd || j == 0 || j == 3; }
 
+// out[j] = v of lane j of this 16-lane row (the row's lanes 0-3 each computed
+// one component of a 4-vector; the row must be converged)
+__device__ __forceinline__ void row4(double v, double out[4]) {
+  out[0] = rowb<0>(v);
+  out[1] = rowb<1>(v);
+  out[2] = rowb<2>(v);
+  out[3] = rowb<3>(v);
+}
+
 // ---------------------------------------------------------------------------
 // potential (oracle: nuts_potential), row-collective
 // ---------------------------------------------------------------------------
@@ -296,6 +305,7 @@ struct ChainState {
   double s_w, s_rsum[4], s_acc;
   int s_n, n_leaf, nmax;
   bool s_div;
+  int ul_chunk;  // chunk of leaf uniforms in sul (-1: none)
   // statistics of the kept iterations
   double st_div, st_leap;
 };
@@ -325,6 +335,7 @@ __device__ __forceinline__ void chain_init(ChainState& c) {
   c.s_n = c.n_leaf = 0;
   c.nmax = 1;
   c.s_div = false;
+  c.ul_chunk = -1;
   c.st_div = c.st_leap = 0.0;
 }
 
@@ -343,8 +354,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   __shared__ RowState srow[4];
   __shared__ ChainState schain[4];
   __shared__ double sck[8][kWave];  // checkpoint i of a row on its lane i: r[4], rsum[4]
+  // draws of the current iteration computed one per lane, in parallel: lane j
+  // of a row holds doubling j's direction bit and subtree-merge uniform, and
+  // leaf uniform 16 c + j of the current chunk c (ChainState::ul_chunk)
+  __shared__ double sut[kWave], sul[kWave];
+  __shared__ int sdb[kWave];
   const int lane = threadIdx.x;
   const int r = lane & 31, h = r >> 4, i = r & 15, row = lane >> 4;
+  const int row16 = lane & ~15;
   const int leader = lane & ~31;
   const int qi = blockIdx.x % kQueues;
   // queue qi owns the taxa [tl, tl + nq) and serves their 4 nq tasks heaviest
@@ -586,7 +603,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       } else {
         const double nw = logaddexp(s_w, w);
         const double prob = exp(w - nw);
-        if (uniform(st, (uint32_t)it, 32u + (uint32_t)leaf_ctr) < prob) {
+        if ((leaf_ctr >> 4) != C.ul_chunk) {  // next 16 leaf uniforms, one per lane
+          sul[lane] = uniform(st, (uint32_t)it, 32u + (uint32_t)(leaf_ctr & ~15) + (uint32_t)i);
+          C.ul_chunk = leaf_ctr >> 4;
+        }
+        if (sul[row16 + (leaf_ctr & 15)] < prob) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             R.sz[j] = zev[j];
@@ -723,8 +744,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         } else {
           // next doubling
           const int j = t_depth;
-          right = (block(st, (uint32_t)it, 4u + 2u * (uint32_t)j).x & 1u) != 0u;
-          u_tr = uniform(st, (uint32_t)it, 5u + 2u * (uint32_t)j);
+          right = sdb[row16 + j] != 0;
+          u_tr = sut[row16 + j];
           n_leaf = 0;
           nmax = 1 << j;
           step = right ? eps : -eps;
@@ -749,11 +770,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       }
       if (mode != kFind) mode = kFind;
       eps = ldexp(eps, f_dir);
+      // the 4 momentum draws in parallel: lane j of the row draws component j
+      double nj[4];
+      row4(normal(st, 0xFFFE0000u + 4096u * (uint32_t)f_call + (uint32_t)f_m, (uint32_t)(i & 3)), nj);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        pr[j] = active(pd.pmd, j)
-                    ? normal(st, 0xFFFE0000u + 4096u * (uint32_t)f_call + (uint32_t)f_m, (uint32_t)j) * sqrt(1.0 / invm[j])
-                    : 0.0;
+        pr[j] = active(pd.pmd, j) ? nj[j] * sqrt(1.0 / invm[j]) : 0.0;
         pz[j] = R.tz[j];
         pg[j] = R.tg[j];
       }
@@ -762,9 +784,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
     }
     if (begin_iter) {
       mode = kIter;
+      double nj[4];
+      row4(normal(st, (uint32_t)it, (uint32_t)(i & 3)), nj);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        pr[j] = active(pd.pmd, j) ? normal(st, (uint32_t)it, (uint32_t)j) * sqrt(1.0 / invm[j]) : 0.0;
+        pr[j] = active(pd.pmd, j) ? nj[j] * sqrt(1.0 / invm[j]) : 0.0;
         pz[j] = R.tz[j];
         pg[j] = R.tg[j];
         R.lz[j] = R.rz[j] = pz[j];
@@ -780,8 +804,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       t_turn = t_div = false;
       leaf_ctr = 0;
       nleap = 0;
-      right = (block(st, (uint32_t)it, 4u).x & 1u) != 0u;
-      u_tr = uniform(st, (uint32_t)it, 5u);
+      // this iteration's doubling draws, lane j of the row for depth j
+      sdb[lane] = (int)(block(st, (uint32_t)it, 4u + 2u * (uint32_t)i).x & 1u);
+      sut[lane] = uniform(st, (uint32_t)it, 5u + 2u * (uint32_t)i);
+      C.ul_chunk = -1;
+      right = sdb[row16] != 0;
+      u_tr = sut[row16];
       n_leaf = 0;
       nmax = 1;
       step = right ? eps : -eps;
