@@ -85,7 +85,7 @@ def main():
     import torch.distributed as dist
 
     from metadamage_amd import _lib, engine
-    from metadamage_amd.distributed import REC_BYTES, alloc_records, gather_records, packed_views
+    from metadamage_amd.distributed import alloc_records, gather_records
     from metadamage_amd.synthetic import generate
 
     rank = int(os.environ.get("RANK", "0"))
@@ -106,15 +106,15 @@ def main():
     b = generate(T, seed=(2 if nuts else 1) + rank)  # C2 seed 1, C3 seed 2
     ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm, device=dev)
     rec = alloc_records(T, dev)
-    out, pred, status = packed_views(rec, T)
-    res = engine.FitBatch(out, pred, status)
+    out, status = rec.out, rec.status
+    res = engine.FitBatch(rec.out, rec.pred, rec.status)
     opts = _lib.default_opts(mode=_lib.MODE_NUTS if nuts else _lib.MODE_MAP, index_base=rank * T)
     stream = torch.cuda.current_stream(dev)
 
     def step():
         engine.fit_batch_device(ty, tN, tm, opts, res, stream=stream)
         if world > 1:
-            gather_records(rec, T, rank, world)
+            gather_records(rec.stage(), T, rank, world)
 
     for _ in range(args.warmup):
         step()
@@ -151,7 +151,9 @@ def main():
     slot_pe = float(30 * group_evals.sum())
 
     if rank == 0 and nuts:
-        print(json.dumps(nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, b)), flush=True)
+        smp = engine.samples_view(res, T, opts)[:64].cpu().numpy()
+        print(json.dumps(nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, b, smp)),
+              flush=True)
     elif rank == 0:
         total = T * world * args.steps
         value = total / elapsed
@@ -224,7 +226,7 @@ def main():
         dist.destroy_process_group()
 
 
-def nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, b):
+def nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, b, smp):
     """The JSON line of config C3 (the reference's NUTS, 500 warmup + 1000 draws
     per sub-fit, 6 sub-fits per taxon)."""
     from metadamage_amd import _lib
@@ -275,11 +277,44 @@ def nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, 
     }
     if not args.no_cpu_baseline:
         line["cpu_baseline"], ref = cpu_baseline_nuts(b, args.cpu_threads)
-        # full-length chains agree in distribution only: the
-        # deviations are Monte-Carlo scale, not rounding scale
-        line["parity"] = parity(o, st, *ref[::2], kind="distributional (same sampler and Philox streams; "
-                                "full-length chains diverge after a flipped decision, DESIGN.md §9)")
+        line["parity"] = nuts_parity(smp, st, ref)
     return line
+
+
+def _mcse(x, nb=20):
+    """Batch-means Monte-Carlo standard error of the mean along the last axis."""
+    m = x.shape[-1] // nb
+    bm = x[..., : m * nb].reshape(x.shape[:-1] + (nb, m)).mean(-1)
+    return bm.std(-1, ddof=1) / np.sqrt(nb)
+
+
+def nuts_parity(smp, st, ref):
+    """Full-length chains agree with the CPU oracle in distribution only
+    (the dual averaging amplifies last-ulp lnGamma differences
+    until an accept / U-turn decision flips), so parity is measured the way
+    tests/test_gpu_nuts.py does: per taxon, sub-fit and parameter, the
+    difference of the posterior means in units of the combined batch-means
+    MCSE of the two chains.  Same-distribution chains give |z| ~ half-normal
+    (median 0.67)."""
+    ro, rp, rs, rsmp = ref
+    n = len(ro)
+    zs = []
+    for s in range(6):
+        for j in ((0, 1, 2, 3) if s in (0, 2, 3) else (0, 3)):
+            a, r = smp[:n, s, :, j], rsmp[:, s, :, j]
+            se = np.hypot(_mcse(a), _mcse(r))
+            zs.append(np.abs(a.mean(1) - r.mean(1)) / np.maximum(se, 1e-300))
+    z = np.concatenate(zs)
+    return {
+        "kind": "distributional: |posterior mean gpu - cpu| / MCSE over 6 sub-fits x (q, A, c, phi) "
+        "(same sampler and Philox streams; DESIGN.md §9)",
+        "taxa": int(n),
+        "status_match": float((st[:n] == rs).mean()),
+        "median_z": float(np.median(z)),
+        "frac_z_gt_3": float((z > 3).mean()),
+        "max_z": float(z.max()),
+        "within_mc_error": bool(np.median(z) < 1.2 and (z > 5).mean() < 0.03),
+    }
 
 
 def parity(out, st, ref_out, ref_st, kind: str, rtol: float = 1e-4):
@@ -318,7 +353,7 @@ def cpu_baseline_nuts(b, threads: int):
     nthr = threads if threads > 0 else min(16, os.cpu_count() or 1)
     n = 64
     t0 = time.perf_counter()
-    ref = lib.nuts_batch(b.y[:n], b.N[:n], b.mm[:n], threads=nthr)
+    ref = lib.nuts_batch(b.y[:n], b.N[:n], b.mm[:n], threads=nthr, keep_samples=True)
     dt = time.perf_counter() - t0
     n1 = 4
     t1 = time.perf_counter()

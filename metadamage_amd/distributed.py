@@ -18,10 +18,15 @@ import numpy as np
 
 from . import _lib
 
-# bytes of one packed per-taxon record: out f64[NOUT] | pred f32[3*30] | status i32
-REC_OUT = _lib.NOUT * 8
+# One gathered per-taxon record: the result columns of out (f64[NRES_GATHER]:
+# the 25 fields + 7 reserved) | pred f32[3*30] | status i32.  The 48
+# per-sub-fit diagnostic doubles of out stay on the rank that fitted them, so
+# the collective moves 620 instead of 1004 bytes per taxon.
+NRES_GATHER = _lib.F_DIAG
 REC_PRED = _lib.NPRED * _lib.NPOS * 4
-REC_BYTES = REC_OUT + REC_PRED + 4
+REC_RES = NRES_GATHER * 8
+REC_BYTES = REC_PRED + 4 + REC_RES
+REC_OUT = _lib.NOUT * 8  # the full record the kernel writes (rank-local)
 
 
 def shard_range(n_taxa: int, rank: int, world: int) -> tuple[int, int]:
@@ -40,15 +45,36 @@ def shard_capacity(n_taxa: int, world: int) -> int:
     return -(-n_taxa // world) if n_taxa else 0
 
 
+class Records:
+    """Rank-local result buffers of a shard of n taxa: `out` f64[n, NOUT] (the
+    kernel's full record), and one uint8 gather buffer `buf` of n * REC_BYTES
+    bytes holding res f64[n, NRES_GATHER] | pred f32[n, 3, 30] | status i32[n].
+    The kernel writes pred and status in place; `stage()` copies the result
+    columns of out into res (one strided device copy) before the gather."""
+
+    def __init__(self, n: int, device):
+        import torch
+
+        self.n = n
+        self.out = torch.empty((n, _lib.NOUT), dtype=torch.float64, device=device)
+        self.buf = torch.empty(n * REC_BYTES, dtype=torch.uint8, device=device)
+        self.pred, self.status, self.res = packed_views(self.buf, n)
+
+    def stage(self):
+        self.res.copy_(self.out[:, :NRES_GATHER])
+        return self.buf
+
+
 def packed_views(buf, n: int):
-    """Views (out[n, NOUT] f64, pred[n, 3, 30] f32, status[n] i32) into one
-    uint8 record buffer of n * REC_BYTES bytes (torch tensor)."""
-    o1 = n * REC_OUT
+    """Views (pred[n, 3, 30] f32, status[n] i32, res[n, NRES_GATHER] f64) into
+    one uint8 gather buffer of n * REC_BYTES bytes laid out res | pred | status
+    (torch tensor; the f64 block first keeps it 8-byte aligned for any n)."""
+    o1 = n * REC_RES
     o2 = o1 + n * REC_PRED
-    out = buf[:o1].view(dtype=_torch_dtype("float64")).view(n, _lib.NOUT)
+    res = buf[:o1].view(dtype=_torch_dtype("float64")).view(n, NRES_GATHER)
     pred = buf[o1:o2].view(dtype=_torch_dtype("float32")).view(n, _lib.NPRED, _lib.NPOS)
     status = buf[o2 : o2 + 4 * n].view(dtype=_torch_dtype("int32"))
-    return out, pred, status
+    return pred, status, res
 
 
 def _torch_dtype(name):
@@ -57,14 +83,13 @@ def _torch_dtype(name):
     return getattr(torch, name)
 
 
-def alloc_records(n: int, device):
-    import torch
-
-    return torch.empty(n * REC_BYTES, dtype=torch.uint8, device=device)
+def alloc_records(n: int, device) -> Records:
+    return Records(n, device)
 
 
 def gather_records(buf, n_cap: int, rank: int, world: int, group=None):
-    """Gather every rank's record buffer (n_cap records each) to rank 0.
+    """Gather every rank's staged gather buffer (Records.stage(), n_cap records
+    each) to rank 0.
     Returns a list of `world` buffers on rank 0, None elsewhere.  This is the
     one collective of the multi-GPU path (ncclGather semantics)."""
     import torch.distributed as dist
@@ -85,7 +110,7 @@ def unpack_gathered(parts, n_taxa: int, world: int):
     for r, part in enumerate(parts):
         lo, hi = shard_range(n_taxa, r, world)
         n_cap = part.numel() // REC_BYTES
-        o, p, s = packed_views(part, n_cap)
+        p, s, o = packed_views(part, n_cap)
         outs.append(o[: hi - lo].cpu().numpy())
         preds.append(p[: hi - lo].cpu().numpy())
         sts.append(s[: hi - lo].cpu().numpy())

@@ -164,8 +164,7 @@ def fit_packed(p: Packed, opts=None, shard: bool = True):
     import torch
 
     from . import engine
-    from .distributed import alloc_records, gather_records, packed_views, shard_capacity, shard_range
-    from .distributed import unpack_gathered
+    from .distributed import alloc_records, gather_records, shard_capacity, shard_range, unpack_gathered
 
     if not torch.cuda.is_available():
         raise _lib.MdfitError("metadamage_amd fits run on MI355X GPUs only (no HIP device visible)")
@@ -182,13 +181,13 @@ def fit_packed(p: Packed, opts=None, shard: bool = True):
         opts.index_base = opts.index_base + lo
     cap = shard_capacity(p.n_taxa, world)
     rec = alloc_records(cap, dev)
-    out, pred, status = packed_views(rec, cap)
     if hi > lo:
         ty, tN, tm = engine.to_device_counts(p.y[lo:hi], p.N[lo:hi], p.mm[lo:hi], device=dev)
-        engine.fit_batch_device(ty, tN, tm, opts, engine.FitBatch(out[: hi - lo], pred[: hi - lo],
-                                                                   status[: hi - lo]))
+        engine.fit_batch_device(ty, tN, tm, opts, engine.FitBatch(rec.out[: hi - lo], rec.pred[: hi - lo],
+                                                                   rec.status[: hi - lo]))
+    buf = rec.stage()
     torch.cuda.synchronize(dev)
-    parts = gather_records(rec, cap, rank, world)
+    parts = gather_records(buf, cap, rank, world)
     if rank != 0:
         return None
     return unpack_gathered(parts, p.n_taxa, world)

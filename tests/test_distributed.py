@@ -14,7 +14,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from metadamage_amd.distributed import (REC_BYTES, alloc_records, gather_records, packed_views, shard_capacity,
+from metadamage_amd.distributed import (NRES_GATHER, REC_BYTES, alloc_records, gather_records, shard_capacity,
                                         shard_range, unpack_gathered)
 
 
@@ -45,14 +45,14 @@ def _worker(rank, world, port, T, q):
         lo, hi = shard_range(T, rank, world)
         cap = shard_capacity(T, world)
         rec = alloc_records(cap, "cpu")
-        rec.zero_()
-        out, pred, status = packed_views(rec, cap)
+        rec.buf.zero_()
+        rec.out.zero_()
         if hi > lo:
             o, p, s = OracleLib().fit_batch(b.y[lo:hi], b.N[lo:hi], b.mm[lo:hi], threads=1)
-            out[: hi - lo] = torch.from_numpy(o)
-            pred[: hi - lo] = torch.from_numpy(p)
-            status[: hi - lo] = torch.from_numpy(s)
-        parts = gather_records(rec, cap, rank, world)
+            rec.out[: hi - lo] = torch.from_numpy(o)
+            rec.pred[: hi - lo] = torch.from_numpy(p)
+            rec.status[: hi - lo] = torch.from_numpy(s)
+        parts = gather_records(rec.stage(), cap, rank, world)
         if rank == 0:
             q.put(unpack_gathered(parts, T, world))
         else:
@@ -78,16 +78,23 @@ def test_gloo_shard_and_gather_reproduce_single_process(world, T):
         assert p.exitcode == 0
     b = generate(T, seed=8)
     o, pr, s = OracleLib().fit_batch(b.y, b.N, b.mm, threads=1)
-    assert got[0].shape == (T, 80)
-    np.testing.assert_array_equal(got[0], o)
+    # the diagnostic columns stay on the fitting rank: results + reserved only
+    assert got[0].shape == (T, NRES_GATHER)
+    np.testing.assert_array_equal(got[0], o[:, :NRES_GATHER])
     np.testing.assert_array_equal(got[1], pr)
     np.testing.assert_array_equal(got[2], s)
 
 
-def test_record_views_layout():
-    rec = alloc_records(5, "cpu")
-    out, pred, status = packed_views(rec, 5)
-    assert rec.numel() == 5 * REC_BYTES
-    assert out.shape == (5, 80) and pred.shape == (5, 3, 30) and status.shape == (5,)
-    assert out.is_contiguous() and pred.is_contiguous() and status.is_contiguous()
-    assert pred.data_ptr() - out.data_ptr() == 5 * 640
+@pytest.mark.parametrize("n", [5, 6])
+def test_record_views_layout(n):
+    rec = alloc_records(n, "cpu")
+    assert rec.buf.numel() == n * REC_BYTES and REC_BYTES == 620
+    assert rec.out.shape == (n, 80) and rec.res.shape == (n, NRES_GATHER)
+    assert rec.pred.shape == (n, 3, 30) and rec.status.shape == (n,)
+    assert rec.res.is_contiguous() and rec.pred.is_contiguous() and rec.status.is_contiguous()
+    assert rec.res.data_ptr() == rec.buf.data_ptr()
+    assert rec.pred.data_ptr() - rec.buf.data_ptr() == n * NRES_GATHER * 8
+    assert rec.status.data_ptr() - rec.pred.data_ptr() == n * 360
+    rec.out.copy_(torch.arange(n * 80, dtype=torch.float64).view(n, 80))
+    rec.stage()
+    np.testing.assert_array_equal(rec.res.numpy(), rec.out[:, :NRES_GATHER].numpy())
