@@ -33,6 +33,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 
@@ -132,13 +133,39 @@ constexpr int kWsPush = 8, kWsPop = 9, kWsRing = 16;
 // group modes
 constexpr int kIdle = 0, kAllFit = 1, kPairFit = 2, kWaitRing = 3;
 
+// opaque to the optimiser: a rounded value the compiler may not fuse into a
+// later operation (keeps sums bitwise identical across lane layouts)
+__device__ __forceinline__ double opaque(double v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// Lane layouts (PPL = points per lane), bitwise-identical results:
+//  PPL 1: a "slot" = a 32-lane group = 2 rows of 16 (lane = position; row 0
+//         z = 1..15, row 1 z = -1..-15, lane 15 of a row a pad); a pair's
+//         halves are the two rows.  2 slots per wave.
+//  PPL 2: a slot = one 16-lane row.  All-position fit: lane i < 15 holds
+//         z = +(i+1) and z = -(i+1), lane 15 two pads; pair: each 8-lane half
+//         runs one 15-point sub-fit, lane j holding |z| - 1 = 2j, 2j + 1 (lane
+//         7 of a half: 14 and a pad).  4 slots per wave: the Newton logic,
+//         sums and task fetch are shared by twice the points.
+// Sums: every lane first adds its slot partner's point (PPL 1 all-position:
+// the other row, xor 16; PPL 2: its own second point), then one butterfly
+// over the positions in the same tree order, so both layouts give the same
+// bits (and the same fits).
+template <int PPL>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_FIT_WAVES_PER_EU)))
 void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN, int64_t T,
                 int max_iter, double tol, double* __restrict__ out, int* __restrict__ ws) {
+  static_assert(PPL == 1 || PPL == 2, "points per lane");
+  constexpr int kSlot = PPL == 1 ? 32 : 16;  // lanes per slot (one all-position fit or one pair)
+  constexpr int kHalf = kSlot / 2;           // lanes per fwd/rev sub-fit of a pair
   const int lane = threadIdx.x;
-  const int r = lane & 31;       // lane in the 32-lane group
-  const int h = r >> 4;          // half: 0 forward (z > 0), 1 reverse (z < 0)
-  const int leader = lane & ~31;
+  const int r = lane & (kSlot - 1);  // lane in the slot
+  const int h = r / kHalf;           // half: 0 forward (z > 0), 1 reverse (z < 0)
+  const int jh = r & (kHalf - 1);    // lane in the half
+  const int leader = lane & ~(kSlot - 1);
+  const unsigned long long slot_mask = (kSlot == 32 ? 0xFFFFFFFFull : 0xFFFFull) << leader;
   const int qi = blockIdx.x % kQueues;
   const int64_t nall = 2 * T;  // all-position tasks: (taxon, model)
   // queue qi owns the taxa [tl, tl + nq): first their PMD fits (the long ones,
@@ -146,21 +173,42 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
   const int64_t tl = T * qi / kQueues, nq = T * (qi + 1) / kQueues - tl;
   int* ring = ws + kWsRing;
 
-  // this lane's position: column h*15 + i, |z|-1 = i (lane i = 15 of a half is a pad)
-  PointData pd;
-  {
-    const int i = r & 15;
-    pd.valid = i < kNHalf;
-    pd.k = pd.valid ? i : 0;
+  // this lane's point(s).  Columns: col c of a taxon row is z = c+1 (c < 15)
+  // or z = -(c-14); |z|-1 = k.  Per mode (all / pair) the points differ for
+  // PPL 2; pads carry y = N = 0.
+  PointData pa, pb;
+  int colA_all = 0, colA_pair = 0, colB_all = 0, colB_pair = 0;
+  bool vA_all, vA_pair, vB_all = false, vB_pair = false;
+  int kA_all, kA_pair, kB_all = 0, kB_pair = 0;
+  if (PPL == 1) {
+    const int i = r & 15;  // lane in its row = |z|-1
+    vA_all = vA_pair = i < kNHalf;
+    kA_all = kA_pair = vA_all ? i : 0;
+    colA_all = colA_pair = vA_all ? h * kNHalf + i : 0;
+  } else {
+    vA_all = vB_all = r < kNHalf;
+    kA_all = kB_all = vA_all ? r : 0;
+    colA_all = vA_all ? r : 0;
+    colB_all = vA_all ? kNHalf + r : 0;
+    kA_pair = 2 * jh;
+    kB_pair = 2 * jh + 1;
+    vA_pair = true;
+    vB_pair = kB_pair < kNHalf;
+    kB_pair = vB_pair ? kB_pair : 0;
+    colA_pair = h * kNHalf + kA_pair;
+    colB_pair = vB_pair ? h * kNHalf + kB_pair : 0;
   }
-  const int col = pd.valid ? h * kNHalf + pd.k : 0;
-  pd.y = pd.N = 0.0;
-  pd.pmd = true;
+  pa.y = pa.N = pb.y = pb.N = 0.0;
+  pa.valid = vA_all;
+  pa.k = kA_all;
+  pb.valid = vB_all;
+  pb.k = kB_all;
+  pa.pmd = pb.pmd = true;
 
   int mode = kIdle, slot = 0, pollv = 0;
   bool polled = false, publish = false;
   bool all_drained = false, ring_drained = false;
-  // the sub-fit of this lane's half (replicated on its 16 lanes; for an
+  // the sub-fit of this lane's half (replicated on its lanes; for an
   // all-position fit both halves hold identical state)
   int64_t taxon = 0;
   int sub = 0;
@@ -180,7 +228,7 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
     const unsigned long long f0 = stamp();
 #endif
     bool starting = false;
-    // ---- 1. idle groups pull an all-position task (one atomic per wave-trip) --
+    // ---- 1. idle slots pull an all-position task (one atomic per wave-trip) ---
     const bool need1 = mode == kIdle && !all_drained;
 #ifdef MDFIT_STAMP
     const unsigned long long a0 = stamp();
@@ -224,7 +272,7 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
 #ifdef MDFIT_STAMP
     st_claim2 += stamp() - a1;
 #endif
-    // a waiting group reads the poll it issued last trip (relaxed, its latency
+    // a waiting slot reads the poll it issued last trip (relaxed, its latency
     // hidden behind that trip's evaluation); the acquire fence then makes the
     // pair's u0, written before the producer's release, visible
     const bool ready = mode == kWaitRing && polled && pollv != 0;
@@ -237,9 +285,20 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       starting = true;
     }
     if (starting) {
-      pd.pmd = sub == 0 || sub == 2 || sub == 3;
-      pd.y = pd.valid ? (double)gy[taxon * kLD + col] : 0.0;
-      pd.N = pd.valid ? (double)gN[taxon * kLD + col] : 0.0;
+      const bool whole_s = mode == kAllFit;
+      pa.pmd = pb.pmd = sub == 0 || sub == 2 || sub == 3;
+      pa.valid = whole_s ? vA_all : vA_pair;
+      pa.k = whole_s ? kA_all : kA_pair;
+      const int ca = whole_s ? colA_all : colA_pair;
+      pa.y = pa.valid ? (double)gy[taxon * kLD + ca] : 0.0;
+      pa.N = pa.valid ? (double)gN[taxon * kLD + ca] : 0.0;
+      if (PPL == 2) {
+        pb.valid = whole_s ? vB_all : vB_pair;
+        pb.k = whole_s ? kB_all : kB_pair;
+        const int cb = whole_s ? colB_all : colB_pair;
+        pb.y = pb.valid ? (double)gy[taxon * kLD + cb] : 0.0;
+        pb.N = pb.valid ? (double)gN[taxon * kLD + cb] : 0.0;
+      }
       const double* dg = diag(out, taxon, sub);  // u0: K0 init, or the all-position mode
 #pragma unroll
       for (int j = 0; j < 4; ++j) u[j] = ut[j] = dg[j];
@@ -257,27 +316,51 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
 #endif
     polled = mode == kWaitRing;
     if (polled) pollv = __hip_atomic_load(ring + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!__any(running)) {  // only waiting groups: back off briefly
+    if (!__any(running)) {  // only waiting slots: back off briefly
       __builtin_amdgcn_s_sleep(8);
       continue;
     }
 
     // ---- 3. value + gradient + Hessian at the trial point --------------------
-    const Theta th = make_theta(pd.pmd, ut);  // row-collective: every lane
+    const bool whole = mode == kAllFit;
+    const Theta th = make_theta<kHalf>(pa.pmd, ut);  // row-collective: every lane
     double acc[kNAcc];
 #pragma unroll
     for (int j = 0; j < kNAcc; ++j) acc[j] = 0.0;
-    point_accum<true>(pd, th, acc);
+    if (PPL == 1) {
+      point_accum<true>(pa, th, acc);
+    } else {
+      // lg3(phi) from a pad: lane 15's point b (all-position: both halves;
+      // pair: the reverse half), lane 7's point b (pair: the forward half)
+      const LG3 t3b = lg3(pb.N + th.phi);
+      const bool src15 = whole || h == 1;
+      LG3 t6;
+      t6.l = src15 ? rowb<15>(t3b.l) : rowb<7>(t3b.l);
+      t6.p = src15 ? rowb<15>(t3b.p) : rowb<7>(t3b.p);
+      t6.q = src15 ? rowb<15>(t3b.q) : rowb<7>(t3b.q);
+      point_contrib(pa, th, lg3(pa.N + th.phi), t6, acc);
+      double accb[kNAcc];
+#pragma unroll
+      for (int j = 0; j < kNAcc; ++j) accb[j] = 0.0;
+      point_contrib(pb, th, t3b, t6, accb);
+#pragma unroll
+      for (int j = 0; j < kNAcc; ++j) acc[j] = opaque(acc[j]) + opaque(accb[j]);
+    }
 #ifdef MDFIT_STAMP
     const unsigned long long e1 = stamp();
 #endif
-    // sums over the half (16 lanes); all-position fits add the other half
-    const bool whole = mode == kAllFit;
+    // sums over the slot's positions (all-position fits) or the half's
 #pragma unroll
     for (int j = 0; j < kNAcc; ++j) {
-      const double s16 = gsum<16>(acc[j]);
-      const double s32 = s16 + __shfl_xor(s16, 16, 64);
-      acc[j] = whole ? s32 : s16;
+      if (PPL == 1) {
+        const double v = opaque(acc[j]);
+        const double o = __shfl_xor(v, 16, 64);
+        acc[j] = gsum<16>(whole ? v + o : v);
+      } else {
+        const double s8 = gsum<8>(acc[j]);
+        const double s16 = s8 + dpp<0x140>(s8);  // row_mirror: the other half's sum
+        acc[j] = whole ? s16 : s8;
+      }
     }
 #ifdef MDFIT_STAMP
     const unsigned long long e2 = stamp();
@@ -286,7 +369,7 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
     // ---- 4. Newton logic (oracle: fit_one) ----------------------------------
     if (running) {
       Eval tr;
-      finish_eval(pd.pmd, th, acc, tr);
+      finish_eval(pa.pmd, th, acc, tr);
       ++evals;
       bool accept, done = false;
       if (first) {
@@ -308,7 +391,7 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         curMag = tr.mag;
         curPg = pgnorm(u, tr.g);
         if (!done) {
-          newton_dir(pd.pmd, u, tr.g, tr.H, d);
+          newton_dir(pa.pmd, u, tr.g, tr.H, d);
           t = 1.0;
           if (maxabs4(d) <= tol) {
             done = true;
@@ -333,15 +416,15 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         // lanes 0..7 of the half write the diag slots (for an all-position fit
         // the forward half only); a converged all-position fit also seeds the
         // u0 of its forward / reverse fits, then releases that pair
-        const int i = r & 15;
+        const int i = jh;
         const bool writer = (!whole || h == 0) && i < 8;
         if (writer) {
           const double v = i < 4 ? sel4(u, i)
                                  : (i == 4 ? curF : (i == 5 ? (double)evals : (i == 6 ? (double)status : 0.0)));
           diag(out, taxon, sub)[i] = v;
           if (whole && status == MDFIT_OK && i < 4) {
-            diag(out, taxon, pd.pmd ? 2 : 4)[i] = v;
-            diag(out, taxon, pd.pmd ? 3 : 5)[i] = v;
+            diag(out, taxon, pa.pmd ? 2 : 4)[i] = v;
+            diag(out, taxon, pa.pmd ? 3 : 5)[i] = v;
           }
         }
         publish = whole && r == 0;
@@ -363,9 +446,15 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       }
       publish = false;
     }
-    // a group is free when neither half is running
+#ifdef MDFIT_PRIO_EVALS
+    // waves holding a long fit (likely on the batch's critical path) win issue
+    // arbitration over waves of short fits
+    if (__any(running && evals >= MDFIT_PRIO_EVALS)) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(0);
+#endif
+    // a slot is free when neither half is running
     const unsigned long long busy = __ballot(running);
-    if (((busy >> leader) & 0xFFFFFFFFull) == 0ull && (mode == kAllFit || mode == kPairFit)) mode = kIdle;
+    if ((busy & slot_mask) == 0ull && (mode == kAllFit || mode == kPairFit)) mode = kIdle;
 #ifdef MDFIT_STAMP
     const unsigned long long l1 = stamp();
     st_fetch += e0 - f0;
@@ -389,6 +478,7 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
   }
 #endif
 }
+
 
 // ---------------------------------------------------------------------------
 // K3: record assembly, one wave per taxon
@@ -724,6 +814,7 @@ using mdfit::host::set_err;
 // per call, events around the whole call and around fit_kernel, on the
 // caller's stream
 constexpr int kProfMax = 256;
+constexpr int64_t kPpl2MinTaxa = 30000;  // measured crossover: 25-30k taxa
 struct ProfState {
   bool on = false;
   int n = 0;
@@ -823,10 +914,21 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   hipLaunchKernelGGL(mdfit::init_kernel, dim3((unsigned)((n_init + 255) / 256)), dim3(256), 0, s, y, N,
                      n_taxa, out);
   if (int rc = check_launch("init_kernel")) return rc;
-  const int64_t g = fit_grid(mdfit::fit_kernel, 2 * n_taxa, 2);
+  // lane layout of the fit kernel (bitwise-identical results): 2 points per
+  // lane for batches that fill the chip several times over, 1 below (lower
+  // latency per evaluation).  MDFIT_FIT_PPL=1|2 overrides (development A/B).
+  int ppl = n_taxa >= kPpl2MinTaxa ? 2 : 1;
+  if (const char* e = std::getenv("MDFIT_FIT_PPL")) ppl = std::atoi(e) == 2 ? 2 : 1;
   prof_record(1, s);
-  hipLaunchKernelGGL(mdfit::fit_kernel, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, y, N, n_taxa,
-                     o.max_iter, o.tol_step, out, ws);
+  if (ppl == 2) {
+    const int64_t g = fit_grid(mdfit::fit_kernel<2>, 2 * n_taxa, 4);
+    hipLaunchKernelGGL(mdfit::fit_kernel<2>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, y, N, n_taxa,
+                       o.max_iter, o.tol_step, out, ws);
+  } else {
+    const int64_t g = fit_grid(mdfit::fit_kernel<1>, 2 * n_taxa, 2);
+    hipLaunchKernelGGL(mdfit::fit_kernel<1>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, y, N, n_taxa,
+                       o.max_iter, o.tol_step, out, ws);
+  }
   if (int rc = check_launch("fit_kernel")) return rc;
   prof_record(2, s);
   hipLaunchKernelGGL(mdfit::assemble_kernel, dim3((unsigned)n_taxa), dim3(mdfit::kWave), 0, s, y, N,

@@ -10,6 +10,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "../../include/mdfit.h"
 #include "mdfit_special.h"
 
@@ -93,13 +95,18 @@ struct Theta {
   double lprior;        // log prior at u (constants dropped)
 };
 
-// Row-collective: every lane of a 16-lane row must be active and hold the
-// same u and model (a row never spans two sub-fits).  The transcendental
-// pieces are spread over the row -- lane 0: sigmoid / log-sigmoids of u0,
-// lane 1: of u1, lane 2: exp(u3) and ln(1-c) -- one exp, one log1p and one
-// reciprocal per lane instead of three of each, then broadcast.
+// Row-collective: every lane of a W-lane row (W = 16: a DPP row; W = 8: one
+// half of a DPP row) must be active and hold the same u and model (a row
+// never spans two sub-fits).  The transcendental pieces are spread over the
+// row -- lane 0: sigmoid / log-sigmoids of u0, lane 1: of u1, lane 2: exp(u3)
+// and ln(1-c) -- one exp, one log1p and one reciprocal per lane instead of
+// three of each, then broadcast (W = 8: from lane 0..2 or 8..10 of the DPP
+// row, by half).  The result does not depend on W.
+template <int W = 16>
 __device__ __forceinline__ Theta make_theta(bool pmd, const double u[4]) {
-  const int i = (int)(threadIdx.x & 15);
+  static_assert(W == 16 || W == 8, "row width");
+  const int i = (int)(threadIdx.x & (W - 1));
+  const bool hi8 = W == 8 && (threadIdx.x & 8);
   const double v = i == 0 ? u[0] : u[1];  // the logit this lane resolves (lanes 0, 1)
   const double e = exp(i < 2 ? -fabs(v) : u[3]);
   const double sp = flog1p(i < 2 ? e : -u[2]);  // ln(1 + e^-|v|), or ln(1-c) on lane 2
@@ -108,13 +115,21 @@ __device__ __forceinline__ Theta make_theta(bool pmd, const double u[4]) {
   const double p = pos ? rr : e * rr, omp = pos ? e * rr : rr;
   // ln p + 2 ln(1-p)  (fits.py:46-48: Beta(2, 3) prior up to a constant)
   const double lpp = (pos ? -sp : v - sp) + 2.0 * (pos ? -(v + sp) : -sp);
+  auto bc = [=](double x, auto n) {
+    constexpr int N = decltype(n)::value;
+    if constexpr (W == 16) return rowb<N>(x);
+    else return hi8 ? rowb<8 + N>(x) : rowb<N>(x);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
   Theta th;
-  th.q = rowb<0>(p);
-  th.omq = rowb<0>(omp);
-  const double lpq = rowb<0>(lpp);
-  const double A = rowb<1>(p), omA = rowb<1>(omp), lpA = rowb<1>(lpp);
-  th.delta = rowb<2>(e);
-  const double l1mc = rowb<2>(sp);
+  th.q = bc(p, I0{});
+  th.omq = bc(omp, I0{});
+  const double lpq = bc(lpp, I0{});
+  const double A = bc(p, I1{}), omA = bc(omp, I1{}), lpA = bc(lpp, I1{});
+  th.delta = bc(e, I2{});
+  const double l1mc = bc(sp, I2{});
   th.iomq = rcp(th.omq);
   th.phi = th.delta + 2.0;
   // ln q + 2 ln(1-q) - delta/1000  [+ ln A + 2 ln(1-A) + 8 ln(1-c)]  (fits.py:46-53)
@@ -155,16 +170,11 @@ struct PointData {
 };
 
 // One point's contribution at theta, ADDED to acc (same formulas as
-// oracle/mdfit_oracle.c evaluate(); derivation in DESIGN.md §3).  Returns the
-// point's log-likelihood (without log C(N,y)).
-//
-// kRowPhi: the (lnGamma, psi, psi1) triple at phi is taken from lane 15 of
-// the 16-lane row -- a pad lane (N = 0) whose lg3(N + phi) IS lg3(phi),
-// bitwise -- so a point costs 5 lg3 instead of 6 (row-collective then: all
-// lanes active, lane 15 of every row a pad holding the row's phi).
-template <bool kRowPhi = false>
-__device__ __forceinline__ double point_accum(const PointData& pd, const Theta& th,
-                                              double acc[kNAcc]) {
+// oracle/mdfit_oracle.c evaluate(); derivation in DESIGN.md §3), given the
+// point's t3 = (lnGamma, psi, psi1)(N + phi) and t6 = the same at phi.
+// Returns the point's log-likelihood (without log C(N,y)).
+__device__ __forceinline__ double point_contrib(const PointData& pd, const Theta& th, const LG3& t3,
+                                               const LG3& t6, double acc[kNAcc]) {
   double D, Dq, DA, Dc, Dqq, DqA;
   if (pd.pmd) {
     const double kk = (double)pd.k;
@@ -194,15 +204,6 @@ __device__ __forceinline__ double point_accum(const PointData& pd, const Theta& 
   const LG3 t5 = lg3(b);
   const double lb = t2.l - t5.l, Pb = t2.p - t5.p, Qb = t2.q - t5.q;
   mag += fabs(t2.l) + fabs(t5.l);
-  const LG3 t3 = lg3(pd.N + phi);
-  LG3 t6;
-  if (kRowPhi) {
-    t6.l = rowb<15>(t3.l);
-    t6.p = rowb<15>(t3.p);
-    t6.q = rowb<15>(t3.q);
-  } else {
-    t6 = lg3(phi);
-  }
   const double lS = t3.l - t6.l, S = t6.p - t3.p, S1 = t6.q - t3.q;
   mag += fabs(t3.l) + fabs(t6.l);
   const double ell = (la + lb) - lS;  // exact 0 when N = 0
@@ -230,6 +231,27 @@ __device__ __forceinline__ double point_accum(const PointData& pd, const Theta& 
     acc[15] += lFF;
   }
   return ell;
+}
+
+// One point's contribution (point_contrib), t3 and t6 computed here.
+//
+// kRowPhi: the (lnGamma, psi, psi1) triple at phi is taken from lane 15 of
+// the 16-lane row -- a pad lane (N = 0) whose lg3(N + phi) IS lg3(phi),
+// bitwise -- so a point costs 5 lg3 instead of 6 (row-collective then: all
+// lanes active, lane 15 of every row a pad holding the row's phi).
+template <bool kRowPhi = false>
+__device__ __forceinline__ double point_accum(const PointData& pd, const Theta& th,
+                                              double acc[kNAcc]) {
+  const LG3 t3 = lg3(pd.N + th.phi);
+  LG3 t6;
+  if (kRowPhi) {
+    t6.l = rowb<15>(t3.l);
+    t6.p = rowb<15>(t3.p);
+    t6.q = rowb<15>(t3.q);
+  } else {
+    t6 = lg3(th.phi);
+  }
+  return point_contrib(pd, th, t3, t6, acc);
 }
 
 // Value-only log-likelihood of one point (lnGamma only; the record assembly

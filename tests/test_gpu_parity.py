@@ -206,3 +206,25 @@ def test_bench_size_properties(engine, oracle_lib):
     ref_out, _, ref_st = oracle_lib.fit_batch(b.y[idx], b.N[idx], b.mm[idx])
     assert (ref_st == st1[idx]).all()
     assert mixed_rel(out1[idx, :25], ref_out[:, :25]).max() < RTOL
+
+
+def test_lane_layouts_are_bitwise_identical(engine, monkeypatch):
+    """The fit kernel's two lane layouts (1 point per lane below 30k taxa, 2
+    above) sum in the same tree order, so a taxon's record does
+    not depend on the batch size that picked the layout."""
+    from metadamage_amd.synthetic import generate
+
+    b = generate(3_000, seed=11)
+    res = {}
+    for ppl in ("1", "2"):
+        monkeypatch.setenv("MDFIT_FIT_PPL", ppl)
+        res[ppl] = engine.fit_batch(b.y, b.N, b.mm)
+    for a, c in zip(res["1"], res["2"]):
+        assert np.array_equal(a, c, equal_nan=True)
+    # and a taxon fitted inside a batch above the threshold matches it too
+    monkeypatch.delenv("MDFIT_FIT_PPL")
+    more = generate(28_000, seed=12)
+    cat = [np.concatenate([getattr(b, f), getattr(more, f)]) for f in ("y", "N", "mm")]
+    out_big, pred_big, st_big = engine.fit_batch(*cat)
+    assert np.array_equal(out_big[:3_000], res["1"][0], equal_nan=True)
+    assert np.array_equal(pred_big[:3_000], res["1"][1], equal_nan=True)
