@@ -14,20 +14,16 @@
 //                              the 6 modes, n_sigma x3, asymmetry, predictive
 //                              summaries, sums, noise (fits.py:230-376)
 //
-// K1 work decomposition: a wave = 2 groups of 32 lanes, a group = 2 halves of
-// 16 lanes, lane = position (half 0: z = 1..15, half 1: z = -1..-15, lane 15
-// of a half is a pad).  A group runs either one all-position sub-fit (the
-// halves' sums added: both hold identical Newton state) or the forward /
-// reverse pair of one model (each half its own Newton state machine).  Per
-// trip every running fit evaluates value + gradient + Hessian at its trial
-// point (one point per lane, then a DPP butterfly) and runs its Newton logic.
-// Free groups pull all-position tasks from 8 per-XCD queues (one atomic per
-// wave-trip); once those are drained they take fwd/rev pairs from a ready
-// ring that each finished all-position fit appends its pair to (release /
-// acquire at agent scope: the pair's warm-start u0 is in the record), so the
-// pairs of early taxa run while the last all-position fits are still going.
+// K1 work decomposition (details at fit_kernel): lane = position; a "slot"
+// (32 lanes at 1 point per lane, 16 at 2) runs either one all-position
+// sub-fit (both halves hold identical Newton state) or the forward / reverse
+// pair of one model (each half its own Newton state machine).  Per trip every
+// running fit evaluates value + gradient + Hessian at its trial point (then a
+// DPP butterfly) and runs its Newton logic.  Free slots pull all-position
+// tasks from 8 per-XCD queues (one atomic per wave-trip) and continue in
+// place with the task's fwd/rev pair, warm-started at the all-position mode.
 // (Claiming one task ahead to hide the atomic + load latency was measured
-// slower: the last tasks then queue behind long fits while other groups sit
+// slower: the last tasks then queue behind long fits while other slots sit
 // idle.)  Everything is FP64 (the reference enables x64, fits.py:32).
 #include <hip/hip_runtime.h>
 
@@ -46,7 +42,7 @@ namespace mdfit {
 
 constexpr int kAll = 0, kFR = 1;
 
-// diag slots of the out record (include/mdfit.h): during K1/K2 slots 0..3 of a
+// diag slots of the out record (include/mdfit.h): during K1 slots 0..3 of a
 // sub-fit hold its unconstrained mode u*, K3 turns them into (q, A, c, phi)
 __device__ __forceinline__ double* diag(double* out, int64_t taxon, int sub) {
   return out + taxon * MDFIT_NOUT + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * sub;
@@ -126,12 +122,10 @@ __global__ __launch_bounds__(256) void init_kernel(const uint32_t* __restrict__ 
 #define MDFIT_FIT_WAVES_PER_EU 2
 #endif
 
-// workspace layout (int32): [0, 8) per-XCD all-position task counters,
-// [8] ring push counter, [9] ring pop counter, [16, 16 + 2T) ready ring
-constexpr int kWsPush = 8, kWsPop = 9, kWsRing = 16;
+// workspace layout (int32): [0, kQueues) per-XCD all-position task counters
 
-// group modes
-constexpr int kIdle = 0, kAllFit = 1, kPairFit = 2, kWaitRing = 3;
+// slot modes
+constexpr int kIdle = 0, kAllFit = 1, kPairFit = 2, kNextPair = 3;
 
 // opaque to the optimiser: a rounded value the compiler may not fuse into a
 // later operation (keeps sums bitwise identical across lane layouts)
@@ -153,6 +147,13 @@ __device__ __forceinline__ double opaque(double v) {
 // the other row, xor 16; PPL 2: its own second point), then one butterfly
 // over the positions in the same tree order, so both layouts give the same
 // bits (and the same fits).
+//
+// Work: a free slot claims an all-position task (taxon, model) from its
+// XCD's queue (PMD tasks first: the long ones), fits it, then continues in
+// place with the forward / reverse pair of the same taxon and model, warm-
+// started at the all-position mode (still in registers; the counts too --
+// PPL 2 re-deals them to the pair layout with lane shuffles), so a pair costs
+// no memory round trip and no hand-off between waves.
 template <int PPL>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_FIT_WAVES_PER_EU)))
 void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN, int64_t T,
@@ -167,37 +168,36 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
   const int leader = lane & ~(kSlot - 1);
   const unsigned long long slot_mask = (kSlot == 32 ? 0xFFFFFFFFull : 0xFFFFull) << leader;
   const int qi = blockIdx.x % kQueues;
-  const int64_t nall = 2 * T;  // all-position tasks: (taxon, model)
-  // queue qi owns the taxa [tl, tl + nq): first their PMD fits (the long ones,
-  // which also release the long fwd/rev pairs), then their null fits
+  // queue qi owns the taxa [tl, tl + nq): first their PMD fits (the long ones),
+  // then their null fits
   const int64_t tl = T * qi / kQueues, nq = T * (qi + 1) / kQueues - tl;
-  int* ring = ws + kWsRing;
 
   // this lane's point(s).  Columns: col c of a taxon row is z = c+1 (c < 15)
   // or z = -(c-14); |z|-1 = k.  Per mode (all / pair) the points differ for
   // PPL 2; pads carry y = N = 0.
   PointData pa, pb;
-  int colA_all = 0, colA_pair = 0, colB_all = 0, colB_pair = 0;
   bool vA_all, vA_pair, vB_all = false, vB_pair = false;
-  int kA_all, kA_pair, kB_all = 0, kB_pair = 0;
+  int kA_all, kA_pair, kB_all = 0, kB_pair = 0, colA_all;
   if (PPL == 1) {
     const int i = r & 15;  // lane in its row = |z|-1
     vA_all = vA_pair = i < kNHalf;
     kA_all = kA_pair = vA_all ? i : 0;
-    colA_all = colA_pair = vA_all ? h * kNHalf + i : 0;
+    colA_all = vA_all ? h * kNHalf + i : 0;
   } else {
     vA_all = vB_all = r < kNHalf;
     kA_all = kB_all = vA_all ? r : 0;
     colA_all = vA_all ? r : 0;
-    colB_all = vA_all ? kNHalf + r : 0;
     kA_pair = 2 * jh;
     kB_pair = 2 * jh + 1;
     vA_pair = true;
     vB_pair = kB_pair < kNHalf;
     kB_pair = vB_pair ? kB_pair : 0;
-    colA_pair = h * kNHalf + kA_pair;
-    colB_pair = vB_pair ? h * kNHalf + kB_pair : 0;
   }
+  // PPL 2 pair layout: lane j of half h takes the counts at |z|-1 = 2j, 2j+1
+  // of its direction from lanes 2j, 2j+1 of the all-position layout (point a
+  // = forward, point b = reverse there)
+  const int srcA = leader + (PPL == 2 ? kA_pair : 0);
+  const int srcB = leader + (PPL == 2 ? (vB_pair ? kB_pair : 0) : 0);
   pa.y = pa.N = pb.y = pb.N = 0.0;
   pa.valid = vA_all;
   pa.k = kA_all;
@@ -205,9 +205,8 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
   pb.k = kB_all;
   pa.pmd = pb.pmd = true;
 
-  int mode = kIdle, slot = 0, pollv = 0;
-  bool polled = false, publish = false;
-  bool all_drained = false, ring_drained = false;
+  int mode = kIdle;
+  bool drained = false, allok = false;
   // the sub-fit of this lane's half (replicated on its lanes; for an
   // all-position fit both halves hold identical state)
   int64_t taxon = 0;
@@ -229,7 +228,7 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
 #endif
     bool starting = false;
     // ---- 1. idle slots pull an all-position task (one atomic per wave-trip) ---
-    const bool need1 = mode == kIdle && !all_drained;
+    const bool need1 = mode == kIdle && !drained;
 #ifdef MDFIT_STAMP
     const unsigned long long a0 = stamp();
 #endif
@@ -241,12 +240,26 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       if (need1) {
         const int64_t task = (int64_t)base + __popcll(m & ((1ull << leader) - 1ull));
         if (task >= 2 * nq) {
-          all_drained = true;
+          drained = true;
         } else {
           sub = task < nq ? 0 : 1;  // 0 PMD-all, 1 null-all
           taxon = tl + task - (sub ? nq : 0);
           mode = kAllFit;
           starting = true;
+          pa.pmd = pb.pmd = sub == 0;
+          pa.valid = vA_all;
+          pa.k = kA_all;
+          pa.y = pa.valid ? (double)gy[taxon * kLD + colA_all] : 0.0;
+          pa.N = pa.valid ? (double)gN[taxon * kLD + colA_all] : 0.0;
+          if (PPL == 2) {
+            pb.valid = vB_all;
+            pb.k = kB_all;
+            pb.y = pb.valid ? (double)gy[taxon * kLD + kNHalf + colA_all] : 0.0;
+            pb.N = pb.valid ? (double)gN[taxon * kLD + kNHalf + colA_all] : 0.0;
+          }
+          const double* dg = diag(out, taxon, sub);  // u0 from K0
+#pragma unroll
+          for (int j = 0; j < 4; ++j) u[j] = dg[j];
         }
       }
     }
@@ -254,54 +267,42 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
     const unsigned long long a1 = stamp();
     st_claim1 += a1 - a0;
 #endif
-    // ---- 2. then fwd/rev pairs, released by finished all-position fits -------
-    const bool need2 = mode == kIdle && all_drained && !ring_drained;
-    if (__any(need2)) {
-      int j = 0;
-      if (need2 && r == 0) j = atomicAdd(ws + kWsPop, 1);
-      j = __shfl(j, leader);
-      if (need2) {
-        if (j >= nall) {
-          ring_drained = true;
-        } else {
-          slot = j;
-          mode = kWaitRing;
+    // ---- 2. a finished all-position fit continues with its fwd/rev pair ----
+    const bool next = mode == kNextPair;
+    if (__any(next)) {
+      if (PPL == 2) {  // wave-wide: every lane takes part in the shuffles
+        const double ya = __shfl(pa.y, srcA), Na = __shfl(pa.N, srcA);
+        const double yb = __shfl(pb.y, srcA), Nb = __shfl(pb.N, srcA);
+        const double ya2 = __shfl(pa.y, srcB), Na2 = __shfl(pa.N, srcB);
+        const double yb2 = __shfl(pb.y, srcB), Nb2 = __shfl(pb.N, srcB);
+        if (next) {
+          pa.valid = vA_pair;
+          pa.k = kA_pair;
+          pa.y = h ? yb : ya;
+          pa.N = h ? Nb : Na;
+          pb.valid = vB_pair;
+          pb.k = kB_pair;
+          pb.y = vB_pair ? (h ? yb2 : ya2) : 0.0;
+          pb.N = vB_pair ? (h ? Nb2 : Na2) : 0.0;
         }
+      }
+      if (next) {
+        sub = (pa.pmd ? 2 : 4) + h;  // PMD-f/r or null-f/r
+        mode = kPairFit;
+        starting = true;
+        if (!allok) {  // the all-position fit did not converge: K0's initial point
+          const double* dg = diag(out, taxon, sub);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) u[j] = dg[j];
+        }  // else: warm start at the all-position mode, u
       }
     }
 #ifdef MDFIT_STAMP
     st_claim2 += stamp() - a1;
 #endif
-    // a waiting slot reads the poll it issued last trip (relaxed, its latency
-    // hidden behind that trip's evaluation); the acquire fence then makes the
-    // pair's u0, written before the producer's release, visible
-    const bool ready = mode == kWaitRing && polled && pollv != 0;
-    if (__any(ready)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (ready) {
-      const int64_t task = pollv - 1;
-      taxon = task < T ? task : task - T;
-      sub = task < T ? 2 + h : 4 + h;  // PMD-f/r or null-f/r
-      mode = kPairFit;
-      starting = true;
-    }
     if (starting) {
-      const bool whole_s = mode == kAllFit;
-      pa.pmd = pb.pmd = sub == 0 || sub == 2 || sub == 3;
-      pa.valid = whole_s ? vA_all : vA_pair;
-      pa.k = whole_s ? kA_all : kA_pair;
-      const int ca = whole_s ? colA_all : colA_pair;
-      pa.y = pa.valid ? (double)gy[taxon * kLD + ca] : 0.0;
-      pa.N = pa.valid ? (double)gN[taxon * kLD + ca] : 0.0;
-      if (PPL == 2) {
-        pb.valid = whole_s ? vB_all : vB_pair;
-        pb.k = whole_s ? kB_all : kB_pair;
-        const int cb = whole_s ? colB_all : colB_pair;
-        pb.y = pb.valid ? (double)gy[taxon * kLD + cb] : 0.0;
-        pb.N = pb.valid ? (double)gN[taxon * kLD + cb] : 0.0;
-      }
-      const double* dg = diag(out, taxon, sub);  // u0: K0 init, or the all-position mode
 #pragma unroll
-      for (int j = 0; j < 4; ++j) u[j] = ut[j] = dg[j];
+      for (int j = 0; j < 4; ++j) ut[j] = u[j];
       curF = INFINITY;
       curMag = curPg = 0.0;
       t = 1.0;
@@ -310,16 +311,11 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       first = true;
       running = true;
     }
-    if (!__any(mode != kIdle || !ring_drained)) break;
+    if (!__any(mode != kIdle || !drained)) break;
 #ifdef MDFIT_STAMP
     const unsigned long long e0 = stamp();
 #endif
-    polled = mode == kWaitRing;
-    if (polled) pollv = __hip_atomic_load(ring + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!__any(running)) {  // only waiting slots: back off briefly
-      __builtin_amdgcn_s_sleep(8);
-      continue;
-    }
+    if (!__any(running)) continue;
 
     // ---- 3. value + gradient + Hessian at the trial point --------------------
     const bool whole = mode == kAllFit;
@@ -371,6 +367,7 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       Eval tr;
       finish_eval(pa.pmd, th, acc, tr);
       ++evals;
+      const double pgt = pgnorm(ut, tr.g);  // projected gradient at the trial point
       bool accept, done = false;
       if (first) {
         accept = true;
@@ -381,17 +378,16 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         }
       } else {
         accept = isfinite(tr.F) &&
-                 (tr.F < curF ||
-                  (tr.F <= curF + kNoiseF * (curMag + fabs(curF)) && pgnorm(ut, tr.g) < curPg));
+                 (tr.F < curF || (tr.F <= curF + kNoiseF * (curMag + fabs(curF)) && pgt < curPg));
       }
       if (accept) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) u[j] = ut[j];
         curF = tr.F;
         curMag = tr.mag;
-        curPg = pgnorm(u, tr.g);
+        curPg = pgt;
         if (!done) {
-          newton_dir(pa.pmd, u, tr.g, tr.H, d);
+          newton_dir(pa.pmd, u, tr.g, tr.H, pgt, d);
           t = 1.0;
           if (maxabs4(d) <= tol) {
             done = true;
@@ -414,47 +410,25 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         for (int j = 0; j < 4; ++j) ut[j] = clampd(u[j] + t * d[j], kULo[j], kUHi[j]);
       } else {
         // lanes 0..7 of the half write the diag slots (for an all-position fit
-        // the forward half only); a converged all-position fit also seeds the
-        // u0 of its forward / reverse fits, then releases that pair
+        // the forward half only)
         const int i = jh;
         const bool writer = (!whole || h == 0) && i < 8;
         if (writer) {
           const double v = i < 4 ? sel4(u, i)
                                  : (i == 4 ? curF : (i == 5 ? (double)evals : (i == 6 ? (double)status : 0.0)));
           diag(out, taxon, sub)[i] = v;
-          if (whole && status == MDFIT_OK && i < 4) {
-            diag(out, taxon, pa.pmd ? 2 : 4)[i] = v;
-            diag(out, taxon, pa.pmd ? 3 : 5)[i] = v;
-          }
         }
-        publish = whole && r == 0;
+        allok = status == MDFIT_OK;  // (read after an all-position fit: the pair's warm start)
         running = false;
       }
     }
-    // release the finished all-position fits' fwd/rev pairs (MI355X_MICROARCH
-    // hand-off recipe: stores -> wait -> agent release -> wait -> ticket ->
-    // relaxed flag; the explicit waits keep ROCm 7.2 from dropping the
-    // fence's own wait, which would let the flag overtake the write-back)
-    if (__any(publish)) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (publish) {
-        const int idx = atomicAdd(ws + kWsPush, 1);
-        __hip_atomic_store(ring + idx, (int)(sub * T + taxon) + 1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      }
-      publish = false;
-    }
-#ifdef MDFIT_PRIO_EVALS
-    // waves holding a long fit (likely on the batch's critical path) win issue
-    // arbitration over waves of short fits
-    if (__any(running && evals >= MDFIT_PRIO_EVALS)) __builtin_amdgcn_s_setprio(2);
-    else __builtin_amdgcn_s_setprio(0);
-#endif
-    // a slot is free when neither half is running
+    // a slot is free when neither half is running: an all-position fit then
+    // continues with its pair, a pair with the next task
     const unsigned long long busy = __ballot(running);
-    if ((busy & slot_mask) == 0ull && (mode == kAllFit || mode == kPairFit)) mode = kIdle;
+    if ((busy & slot_mask) == 0ull) {
+      if (mode == kAllFit) mode = kNextPair;
+      else if (mode == kPairFit) mode = kIdle;
+    }
 #ifdef MDFIT_STAMP
     const unsigned long long l1 = stamp();
     st_fetch += e0 - f0;
@@ -490,7 +464,7 @@ __device__ __forceinline__ void predict(double A, double q, double c, double phi
     o[0] = o[1] = o[2] = NAN;
     return;
   }
-  double D = fma(A, pow(1.0 - q, (double)k), c);
+  double D = fma(A, powk(1.0 - q, k), c);
   D = fmin(D, 1.0);
   const double sd = sqrt(D * (1.0 - D) * (phi + N) / (N * (phi + 1.0)));
   o[0] = D;
@@ -541,6 +515,7 @@ __global__ __launch_bounds__(kWave) void assemble_kernel(
   __shared__ double s_y[kLD], s_N[kLD];
   __shared__ uint32_t s_mm[kNPos * kNMM];
   __shared__ double s_rec[MDFIT_NOUT];
+  __shared__ double s_tmp[kWave];
   const int lane = threadIdx.x;
   const int64_t t = blockIdx.x;
   if (t >= n_taxa) return;
@@ -657,7 +632,7 @@ __global__ __launch_bounds__(kWave) void assemble_kernel(
     if (lane == 0) s_rec[MDFIT_F_ASYMMETRY] = (wFR - wC) / sqrt(kNPos * var);
   }
 
-  record_sums_noise(lane, s_y, s_N, s_mm, gmm != nullptr, s_rec);
+  record_sums_noise(lane, s_y, s_N, s_mm, gmm != nullptr, s_rec, s_tmp);
 
   __syncthreads();
   for (int i = lane; i < MDFIT_NOUT; i += kWave) out[t * MDFIT_NOUT + i] = s_rec[i];
@@ -881,8 +856,7 @@ int64_t mdfit_workspace_bytes(int64_t n_taxa, const mdfit_opts* opts) {
   mdfit_default_opts(&o);
   if (opts) o = *opts;
   if (o.mode == MDFIT_MODE_NUTS) return mdfit::nuts::workspace_bytes(n_taxa, o.num_samples);
-  const int64_t b = 4 * (mdfit::kWsRing + 2 * n_taxa);
-  return (b + 255) / 256 * 256;
+  return 256;  // the 8 per-XCD queue counters (int32), padded
 }
 
 int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t n_taxa,
@@ -901,7 +875,7 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   hipStream_t s = (hipStream_t)hip_stream;
   int* ws = (int*)workspace;
   prof_record(0, s);
-  if (hipMemsetAsync(ws, 0, (size_t)(o.mode == MDFIT_MODE_NUTS ? 256 : mdfit_workspace_bytes(n_taxa, &o)), s) !=
+  if (hipMemsetAsync(ws, 0, 256, s) !=
       hipSuccess)
     return check_launch("hipMemsetAsync(workspace)");
   if (o.mode == MDFIT_MODE_NUTS) {

@@ -24,8 +24,8 @@ constexpr int kNMM = MDFIT_NMM;
 constexpr double kZ68 = 0.994457883209753;  // Phi^-1(0.84)
 
 // u = (logit q, logit A, c, log delta): c on its own scale (see oracle).
-__constant__ double kULo[4] = {-25.0, -25.0, 0.0, -25.0};
-__constant__ double kUHi[4] = {25.0, 25.0, 0.999, 20.0};
+constexpr double kULo[4] = {-25.0, -25.0, 0.0, -25.0};
+constexpr double kUHi[4] = {25.0, 25.0, 0.999, 20.0};
 constexpr double kEpsAct = 1e-8;
 constexpr double kNoiseF = 1.4e-14;  // objective rounding scale (oracle: NOISE_F)
 constexpr double kPgTol = 1e-6;      // exhausted line search + |proj. grad| below: converged (oracle: PG_TOL)
@@ -319,7 +319,16 @@ __device__ __forceinline__ double pgnorm(const double u[4], const double g[4]) {
   return m;
 }
 
-__constant__ double kEpsBind[4] = {1e-3, 1e-3, 1e-4, 1e-3};
+constexpr double kEpsBind[4] = {1e-3, 1e-3, 1e-4, 1e-3};
+
+// 1/sqrt(x), x > 0: v_rsq_f64 + two Newton steps (no IEEE sqrt sequence)
+__device__ __forceinline__ double rsqrt_nr(double x) {
+  double r = __builtin_amdgcn_rsq(x);
+  const double hx = 0.5 * x;
+  r = r * fma(-hx * r, r, 1.5);
+  r = r * fma(-hx * r, r, 1.5);
+  return r;
+}
 
 // Cholesky of the free block of H + mu*I (fixed / bound rows -> identity);
 // false if a pivot is not positive.  Packed lower triangle L (same index as
@@ -338,9 +347,10 @@ __device__ __forceinline__ bool chol4(const bool fr[4], const double H[10], doub
       for (int p = 0; p < m; ++p) s -= L[hidx(p, j)] * L[hidx(p, m)];
       if (j == m) {
         if (!(s > 0.0)) ok = false;
-        const double lj = sqrt(fmax(s, 1e-300));
-        L[hidx(j, j)] = lj;
-        iL[j] = rcp(lj);
+        const double sp = fmax(s, 1e-300);
+        const double il = rsqrt_nr(sp);  // 1/L_jj, then L_jj = s/L_jj
+        L[hidx(j, j)] = sp * il;
+        iL[j] = il;
       } else {
         L[hidx(m, j)] = s * iL[m];  // L(j,m) stored at packed (m,j)
       }
@@ -352,16 +362,12 @@ __device__ __forceinline__ bool chol4(const bool fr[4], const double H[10], doub
 // Projected, Hessian-modified Newton direction with a Bertsekas binding set
 // (oracle: direction()): variables within eps of a bound and pushed outward
 // step onto the bound and leave the Newton system.
+// w = pgnorm(u, g) (the fixed coordinates of model_null have g = 0 and sit
+// inside the box, so they add nothing to it).
 __device__ __forceinline__ void newton_dir(bool pmd, const double u[4], const double g[4],
-                                           const double H[10], double d[4]) {
+                                           const double H[10], double w, double d[4]) {
   bool fr[4];
   double dbind[4];
-  double w = 0.0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const bool fixed = !pmd && (j == 1 || j == 2);
-    if (!fixed) w = fmax(w, fabs(u[j] - clampd(u[j] - g[j], kULo[j], kUHi[j])));
-  }
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const bool fixed = !pmd && (j == 1 || j == 2);
@@ -423,9 +429,11 @@ __device__ __forceinline__ void newton_dir(bool pmd, const double u[4], const do
 // record pieces shared by the MAP and sampling assembly kernels (one wave per
 // taxon, counts staged in LDS)
 // ---------------------------------------------------------------------------
-// sums (fits.py:272-283) and noise (fits.py:359-376) into the record s_rec
+// sums (fits.py:272-283) and noise (fits.py:359-376) into the record s_rec;
+// s_tmp: 64 doubles of LDS scratch.  Wave-collective (one 64-lane block).
 __device__ __forceinline__ void record_sums_noise(int lane, const double* s_y, const double* s_N,
-                                                  const uint32_t* s_mm, bool has_mm, double* s_rec) {
+                                                  const uint32_t* s_mm, bool has_mm, double* s_rec,
+                                                  double* s_tmp) {
   // ---- sums (fits.py:272-283) -------------------------------------------------
   {
     const double v = lane < kNPos ? 1.0 : 0.0;
@@ -448,24 +456,38 @@ __device__ __forceinline__ void record_sums_noise(int lane, const double* s_y, c
 
   // ---- noise (fits.py:359-376) -------------------------------------------------
   {
-    // lane j < 12 owns mismatch column j (AC AG AT CA CG CT GA GC GT TA TC TG);
-    // CT is NaN on rows 0..14, GA on rows 15..29.
-    const int j = lane < kNMM ? lane : 0;
-    const bool own = lane < kNMM && has_mm;
-    double s = 0.0, cnt = 0.0;
-    for (int i = 0; i < kNPos; ++i) {
+    // mismatch column j = lane % 12 (AC AG AT CA CG CT GA GC GT TA TC TG), rows
+    // i = lane / 12 + 5k (k < 6) on lanes 0..59: 6 rows per lane instead of 30
+    // (shorter dependency chains); CT is NaN on rows 0..14, GA on rows 15..29.
+    constexpr int kG = 5, kRows = kNPos / kG;
+    const int j = lane % kNMM, g = lane / kNMM;
+    const bool own = lane < kNMM * kG && has_mm;
+    const int gi = own ? g : 0;
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < kRows; ++k) {
+      const int i = gi + kG * k;
       const bool nanned = (j == 5 && i < kNHalf) || (j == 6 && i >= kNHalf);
-      if (!nanned) {
-        s += (double)s_mm[i * kNMM + j];
-        cnt += 1.0;
-      }
+      if (!nanned) s += (double)s_mm[i * kNMM + j];
     }
-    const double m = s / cnt;
+    // column sums (exact: integer-valued doubles) through LDS
+    s_tmp[lane] = own ? s : 0.0;
+    __syncthreads();
+    double sc = 0.0;
+#pragma unroll
+    for (int gg = 0; gg < kG; ++gg) sc += s_tmp[j + kNMM * gg];
+    __syncthreads();
+    const double m = sc / ((j == 5 || j == 6) ? (double)kNHalf : (double)kNPos);  // nanmean
     double sa[3] = {0, 0, 0}, ca[3] = {0, 0, 0};
-    for (int i = 0; i < kNPos; ++i) {
+    double xs[kRows];
+#pragma unroll
+    for (int k = 0; k < kRows; ++k) {
+      const int i = gi + kG * k;
       const bool nanned = (j == 5 && i < kNHalf) || (j == 6 && i >= kNHalf);
       const double x = (double)s_mm[i * kNMM + j] / m;
-      if (own && !nanned && !isnan(x)) {
+      const bool use = own && !nanned && !isnan(x);
+      xs[k] = use ? x : NAN;
+      if (use) {
         const int h = i < kNHalf ? 1 : 2;
         sa[0] += x;
         ca[0] += 1.0;
@@ -473,14 +495,18 @@ __device__ __forceinline__ void record_sums_noise(int lane, const double* s_y, c
         ca[h] += 1.0;
       }
     }
-    double mean[3];
+    double mean[3], cq[3];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) mean[q] = gsum<16>(sa[q]) / gsum<16>(ca[q]);
+    for (int q = 0; q < 3; ++q) {
+      cq[q] = gsum<64>(ca[q]);
+      mean[q] = gsum<64>(sa[q]) / cq[q];
+    }
     double ss[3] = {0, 0, 0};
-    for (int i = 0; i < kNPos; ++i) {
-      const bool nanned = (j == 5 && i < kNHalf) || (j == 6 && i >= kNHalf);
-      const double x = (double)s_mm[i * kNMM + j] / m;
-      if (own && !nanned && !isnan(x)) {
+#pragma unroll
+    for (int k = 0; k < kRows; ++k) {
+      const int i = gi + kG * k;
+      const double x = xs[k];
+      if (!isnan(x)) {
         const int h = i < kNHalf ? 1 : 2;
         ss[0] += (x - mean[0]) * (x - mean[0]);
         ss[h] += (x - mean[h]) * (x - mean[h]);
@@ -488,10 +514,7 @@ __device__ __forceinline__ void record_sums_noise(int lane, const double* s_y, c
     }
     double nz[3];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const double c = gsum<16>(ca[q]);
-      nz[q] = c > 0.0 ? sqrt(gsum<16>(ss[q]) / c) : NAN;
-    }
+    for (int q = 0; q < 3; ++q) nz[q] = cq[q] > 0.0 ? sqrt(gsum<64>(ss[q]) / cq[q]) : NAN;
     if (lane == 0) {
       const bool have = has_mm;
       s_rec[MDFIT_F_NORMALIZED_NOISE] = have ? nz[0] : NAN;

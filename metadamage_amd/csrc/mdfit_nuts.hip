@@ -976,6 +976,7 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
   __shared__ double s_y[kLD], s_N[kLD];
   __shared__ uint32_t s_mm[kNPos * kNMM];
   __shared__ double s_rec[MDFIT_NOUT];
+  __shared__ double s_tmp[kWave];
   __shared__ double s_waic[MDFIT_NSUBFIT][kNPos];
   __shared__ double s_v[kMaxSamples];
   const int lane = threadIdx.x;
@@ -1141,7 +1142,7 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
     }
   }
   __syncthreads();
-  record_sums_noise(lane, s_y, s_N, s_mm, gmm != nullptr, s_rec);
+  record_sums_noise(lane, s_y, s_N, s_mm, gmm != nullptr, s_rec, s_tmp);
   __syncthreads();
   for (int x = lane; x < MDFIT_NOUT; x += kWave) out[t * MDFIT_NOUT + x] = s_rec[x];
   if (lane == 0) status[t] = stt;

@@ -47,8 +47,8 @@ def test_abi_version_and_defaults_without_gpu():
     assert (o.seed, o.num_warmup, o.num_samples, o.index_base) == (0, 500, 1000, 0)  # fits.py:792-799
     # the ctypes mirror of mdfit_opts has the C layout (int32, int32, double, uint64, int32, int32, int64)
     assert ctypes.sizeof(_lib.MdfitOpts) == 40
-    # workspace: MAP = queue counters + ready ring; NUTS adds 6 x S x 4 doubles of draws per taxon
-    assert lib.mdfit_workspace_bytes(1000, None) >= 4 * 2000
+    # workspace: MAP = the per-XCD queue counters; NUTS adds 6 x S x 4 doubles of draws per taxon
+    assert lib.mdfit_workspace_bytes(1000, None) >= 4 * 8
     nuts = _lib.default_opts(mode=_lib.MODE_NUTS, num_samples=100)
     assert lib.mdfit_workspace_bytes(1000, ctypes.byref(nuts)) == _lib.SAMPLES_OFFSET + 1000 * 6 * 100 * 4 * 8
 

@@ -39,6 +39,8 @@ def main() -> None:
     b = generate(a.taxa, seed=1)
     ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm)
     res = engine.alloc_outputs(a.taxa)
+    # the workspace size of THIS build (it may differ from the default library's)
+    res.workspace = torch.empty(int(lib.mdfit_workspace_bytes(a.taxa, None)), dtype=torch.uint8, device="cuda")
     stamps = torch.zeros((65536, 8), dtype=torch.int64, device="cuda")
     lib.mdfit_set_stamp(ctypes.c_void_p(stamps.data_ptr()))
     o = _lib.default_opts()

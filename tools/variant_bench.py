@@ -40,6 +40,9 @@ def main() -> None:
     for rep in range(a.reps):
         for path, lib in libs:
             res = engine.alloc_outputs(a.taxa, opts=o)
+            # the workspace size of THIS build (it may differ from the default library's)
+            res.workspace = torch.empty(int(lib.mdfit_workspace_bytes(a.taxa, ctypes.byref(o))), dtype=torch.uint8,
+                                        device="cuda")
 
             def call():
                 _lib.check(lib.mdfit_fit_batch(
