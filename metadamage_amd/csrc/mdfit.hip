@@ -127,13 +127,6 @@ __global__ __launch_bounds__(256) void init_kernel(const uint32_t* __restrict__ 
 // slot modes
 constexpr int kIdle = 0, kAllFit = 1, kPairFit = 2, kNextPair = 3;
 
-// opaque to the optimiser: a rounded value the compiler may not fuse into a
-// later operation (keeps sums bitwise identical across lane layouts)
-__device__ __forceinline__ double opaque(double v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
-
 // Lane layouts (PPL = points per lane), bitwise-identical results:
 //  PPL 1: a "slot" = a 32-lane group = 2 rows of 16 (lane = position; row 0
 //         z = 1..15, row 1 z = -1..-15, lane 15 of a row a pad); a pair's

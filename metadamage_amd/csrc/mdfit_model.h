@@ -61,6 +61,13 @@ __device__ __forceinline__ double gsum(double v) {
   return v;
 }
 
+// opaque to the optimiser: a rounded value the compiler may not fuse into a
+// later operation (keeps sums bitwise identical across lane layouts)
+__device__ __forceinline__ double opaque(double v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 __device__ __forceinline__ double clampd(double x, double lo, double hi) {
   return fmin(fmax(x, lo), hi);
 }
