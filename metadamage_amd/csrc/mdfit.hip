@@ -169,7 +169,9 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
   // or z = -(c-14); |z|-1 = k.  Per mode (all / pair) the points differ for
   // PPL 2; pads carry y = N = 0.
   PointData pa, pb;
-  bool vA_all, vA_pair, vB_all = false, vB_pair = false;
+  // loop-carried per-lane flags are ints (VGPRs): as bools they would be held
+  // in SGPR lane masks, which the compiler spills to VGPR lanes
+  int vA_all, vA_pair, vB_all = 0, vB_pair = 0;
   int kA_all, kA_pair, kB_all = 0, kB_pair = 0, colA_all;
   if (PPL == 1) {
     const int i = r & 15;  // lane in its row = |z|-1
@@ -199,16 +201,16 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
   pa.pmd = pb.pmd = true;
 
   int mode = kIdle;
-  bool drained = false, allok = false;
+  int drained = 0, allok = 0;
   // the sub-fit of this lane's half (replicated on its lanes; for an
   // all-position fit both halves hold identical state)
   int64_t taxon = 0;
   int sub = 0;
-  bool running = false;
+  int running = 0;
   double u[4] = {0, 0, 0, 0}, ut[4] = {0, 0, 0, 0}, d[4] = {0, 0, 0, 0};
   double curF = INFINITY, curMag = 0.0, curPg = 0.0, t = 1.0;
   int evals = 0, status = MDFIT_MAXITER;
-  bool first = true;
+  int first = 1;
 #ifdef MDFIT_STAMP
   unsigned long long st_eval = 0, st_red = 0, st_logic = 0, st_fetch = 0, st_trips = 0;
   unsigned long long st_claim1 = 0, st_claim2 = 0;

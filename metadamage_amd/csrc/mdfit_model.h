@@ -171,9 +171,9 @@ __device__ __forceinline__ double powk(double x, int k) {
 // Per-lane point data of the current phase.
 struct PointData {
   double y, N;
-  int k;       // |z| - 1
-  bool valid;  // a real point (not a pad lane)
-  bool pmd;    // lane group fits model_PMD (else model_null)
+  int k;      // |z| - 1
+  int valid;  // a real point (not a pad lane); ints, not bools: see fit_kernel
+  int pmd;    // lane group fits model_PMD (else model_null)
 };
 
 // One point's contribution at theta, ADDED to acc (same formulas as
