@@ -60,6 +60,7 @@ constexpr double kTarget = 0.8;
 constexpr double kTiny = 2.2250738585072014e-308;
 constexpr double kHuge = 1.7976931348623157e308;
 constexpr int kMaxSamples = 4096;  // LDS bound of the post kernel
+constexpr int kMaxWin = 16;        // adaptation windows (windows() stops at 15 + the terminal one)
 
 // ---------------------------------------------------------------------------
 // Philox4x32-10 and the draw helpers (oracle: philox4x32, nuniform, nnormal)
@@ -246,7 +247,7 @@ __device__ __forceinline__ void ckpt_idxs(int n, int* imin, int* imax) {
 
 __device__ __forceinline__ double logaddexp(double a, double b) {
   const double m = fmax(a, b);
-  return m == -INFINITY ? -INFINITY : m + log1p(exp(-fabs(a - b)));
+  return m == -INFINITY ? -INFINITY : m + flog1p(exp(-fabs(a - b)));
 }
 
 __device__ __forceinline__ bool is_turning(bool pmd, const double invm[4], const double rl[4], const double rr[4],
@@ -428,6 +429,17 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   double& st_leap = C.st_leap;
   chain_init(C);  // every lane of the row writes the same values
   for (int j = 0; j < 8; ++j) sck[j][lane] = 0.0;
+  // the adaptation schedule depends on num_warmup only: window ends once per
+  // wave (lane w < 16 resolves window w) instead of once per transition
+  __shared__ int swin_end[kMaxWin];
+  __shared__ int swin_n;
+  if (lane < kMaxWin) {
+    int e, n;
+    windows(W, lane, &e, &n);
+    swin_end[lane] = e;
+    if (lane == 0) swin_n = n;
+  }
+  __syncthreads();
 #ifdef MDFIT_STAMP
   // [0] top, [1] after the task start, [2] after the potential, [3] after the
   // mode dispatch, [4] end of the body; acc: start, potential, dispatch, begin, trips
@@ -601,8 +613,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         s_acc = acc;
         s_n = 1;
       } else {
-        const double nw = logaddexp(s_w, w);
-        const double prob = exp(w - nw);
+        // nw = logaddexp(s_w, w) and prob = exp(w - nw) from one exp:
+        // prob = 1 / (1 + e^(s_w - w)) (or e/(1+e) when w < s_w)
+        const double m = fmax(s_w, w);
+        const double e = exp(-fabs(s_w - w));
+        const double nw = m == -INFINITY ? -INFINITY : m + flog1p(e);
+        const double prob = (w >= s_w ? 1.0 : e) / (1.0 + e);
         if ((leaf_ctr >> 4) != C.ul_chunk) {  // next 16 leaf uniforms, one per lane
           sul[lane] = uniform(st, (uint32_t)it, 32u + (uint32_t)(leaf_ctr & ~15) + (uint32_t)i);
           C.ul_chunk = leaf_ctr >> 4;
@@ -651,7 +667,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       for (int j = 0; j < 4; ++j) pg[j] = P.g[j];
       if (s_turn || s_div || n_leaf == nmax) {
         // merge the subtree into the tree: biased progressive sampling
-        const double prob = (s_turn || s_div) ? 0.0 : fmin(1.0, exp(s_w - t_w));
+        // prob = min(1, exp(s_w - t_w)) and t_w' = logaddexp(t_w, s_w) from one
+        // exp: for s_w <= t_w, exp(s_w - t_w) = exp(-|t_w - s_w|)
+        const double em = exp(-fabs(t_w - s_w));
+        const double prob = (s_turn || s_div) ? 0.0 : (s_w > t_w ? 1.0 : em);
         if (u_tr < prob) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -674,7 +693,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
             R.lg[j] = pg[j];
           }
         }
-        t_w = logaddexp(t_w, s_w);
+        {
+          const double m = fmax(t_w, s_w);
+          t_w = m == -INFINITY ? -INFINITY : m + flog1p(em);
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) t_rsum[j] += s_rsum[j];
         t_turn = s_turn || (right ? is_turning(pd.pmd, invm, olr, pr, t_rsum) : is_turning(pd.pmd, invm, pr, olr, t_rsum));
@@ -688,14 +710,15 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
           if (it < W) {
             ++t_da;
             const double gg = kTarget - accp;
-            g_avg = (1.0 - 1.0 / (t_da + 10.0)) * g_avg + gg / (t_da + 10.0);
-            const double x_t = mu - sqrt((double)t_da) / 0.05 * g_avg;
-            const double wt = pow((double)t_da, -0.75);
+            const double inv = 1.0 / (t_da + 10.0);
+            g_avg = (1.0 - inv) * g_avg + gg * inv;
+            const double x_t = mu - sqrt((double)t_da) * 20.0 * g_avg;  // / gamma (0.05)
+            const double sq = sqrt((double)t_da);
+            const double wt = 1.0 / (sq * sqrt(sq));  // t^-0.75
             x_avg = (1.0 - wt) * x_avg + wt * x_t;
             eps = exp(it == W - 1 ? x_avg : x_t);
             if (eps < kTiny) eps = kTiny;
-            int wend, nwin;
-            windows(W, widx, &wend, &nwin);
+            const int wend = widx < kMaxWin ? swin_end[widx] : -1, nwin = swin_n;
             const bool middle = widx > 0 && widx < nwin - 1;
             if (middle) {
               ++wn;
