@@ -899,7 +899,7 @@ __device__ double binomial_draw(Draw& d, double n, double p) {
     const double aa = -0.0873 + 0.0248 * bb + 0.01 * pp, cc = n * pp + 0.5;
     const double vr = 0.92 - 4.2 / bb, alpha = (2.83 + 5.1 / bb) * spq;
     const double lpq = log(pp / qq), m = floor((n + 1.0) * pp);
-    const double hh = lgamma(m + 1.0) + lgamma(n - m + 1.0);
+    const double hh = lg3<false>(m + 1.0).l + lg3<false>(n - m + 1.0).l;
     k = floor(cc);
     for (int it = 0; it < 256; ++it) {
       const double u = d.uni() - 0.5, v = d.uni();
@@ -911,7 +911,7 @@ __device__ double binomial_draw(Draw& d, double n, double p) {
         break;
       }
       const double lv = log(v * alpha / (aa / (us * us) + bb));
-      if (lv <= hh - lgamma(kk + 1.0) - lgamma(n - kk + 1.0) + (kk - m) * lpq) {
+      if (lv <= hh - lg3<false>(kk + 1.0).l - lg3<false>(n - kk + 1.0).l + (kk - m) * lpq) {
         k = kk;
         break;
       }
@@ -921,7 +921,7 @@ __device__ double binomial_draw(Draw& d, double n, double p) {
 }
 
 __device__ __forceinline__ double d_at(const double* th, bool pmd, int k) {
-  double D = pmd ? th[1] * pow(1.0 - th[0], (double)k) + th[2] : th[0];
+  double D = pmd ? th[1] * powk(1.0 - th[0], k) + th[2] : th[0];
   return D < 0.0 ? 0.0 : (D > 1.0 ? 1.0 : D);
 }
 
