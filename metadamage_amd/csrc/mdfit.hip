@@ -126,6 +126,7 @@ __global__ __launch_bounds__(256) void init_kernel(const uint32_t* __restrict__ 
 
 // slot modes
 constexpr int kIdle = 0, kAllFit = 1, kPairFit = 2, kNextPair = 3;
+constexpr int kPrioEvals = 15;  // fit length (evaluations) that raises the wave priority
 
 // Lane layouts (PPL = points per lane), bitwise-identical results:
 //  PPL 1: a "slot" = a 32-lane group = 2 rows of 16 (lane = position; row 0
@@ -417,6 +418,12 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         running = false;
       }
     }
+    // waves holding a long fit (the critical path of small batches) win issue
+    // arbitration: +5 % at C2, no change at 100k taxa (A/B of thresholds
+    // 12/15/20/30 and of chain- vs fit-length counting: 15 by fit length best)
+    if (__any(running && evals >= 2 * kPrioEvals)) __builtin_amdgcn_s_setprio(3);
+    else if (__any(running && evals >= kPrioEvals)) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(0);
     // a slot is free when neither half is running: an all-position fit then
     // continues with its pair, a pair with the next task
     const unsigned long long busy = __ballot(running);

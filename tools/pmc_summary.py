@@ -56,8 +56,8 @@ def main() -> None:
     k = "mdfit::fit_kernel"
     fetch_kb = counter_mean(found["pmc_fetch_size.csv"], k, "FETCH_SIZE")
     write_kb = counter_mean(found["pmc_write_size.csv"], k, "WRITE_SIZE")
-    stats = {r["Name"].split("(")[0]: r for r in rows(found["kernel_stats.csv"])}
-    fk = stats.get(k, {})
+    # kernel names as rocprofv3 prints them: "void mdfit::fit_kernel<1>(...)"
+    fk = next((r for r in rows(found["kernel_stats.csv"]) if k in r["Name"].split("(")[0]), {})
     summary = {
         "kernel": k,
         "taxa_per_launch": TAXA,
