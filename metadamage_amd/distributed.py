@@ -87,21 +87,24 @@ def alloc_records(n: int, device) -> Records:
     return Records(n, device)
 
 
-def gather_records(buf, n_cap: int, rank: int, world: int, group=None):
+def gather_records(buf, n_cap: int, rank: int, world: int, group=None, async_op: bool = False):
     """Gather every rank's staged gather buffer (Records.stage(), n_cap records
     each) to rank 0.
     Returns a list of `world` buffers on rank 0, None elsewhere.  This is the
-    one collective of the multi-GPU path (ncclGather semantics)."""
+    one collective of the multi-GPU path (ncclGather semantics).
+
+    async_op=True returns (parts, work) instead: the collective is queued
+    behind the work already on the current stream and runs on the backend's
+    own stream, so the caller can fit the next batch into other buffers while
+    it moves; `work.wait()` orders the current stream after it (and must
+    precede any reuse of `buf` or any read of `parts`)."""
     import torch.distributed as dist
 
     if world == 1:
-        return [buf]
-    if rank == 0:
-        parts = [buf.new_empty(buf.shape) for _ in range(world)]
-        dist.gather(buf, gather_list=parts, dst=0, group=group)
-        return parts
-    dist.gather(buf, dst=0, group=group)
-    return None
+        return ([buf], None) if async_op else [buf]
+    parts = [buf.new_empty(buf.shape) for _ in range(world)] if rank == 0 else None
+    work = dist.gather(buf, gather_list=parts, dst=0, group=group, async_op=async_op)
+    return (parts, work) if async_op else parts
 
 
 def unpack_gathered(parts, n_taxa: int, world: int):

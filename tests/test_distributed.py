@@ -34,7 +34,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, T, q):
+def _worker(rank, world, port, T, q, async_op=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -52,7 +52,21 @@ def _worker(rank, world, port, T, q):
             rec.out[: hi - lo] = torch.from_numpy(o)
             rec.pred[: hi - lo] = torch.from_numpy(p)
             rec.status[: hi - lo] = torch.from_numpy(s)
-        parts = gather_records(rec.stage(), cap, rank, world)
+        if async_op:
+            # bench.py's double-buffered steps: the gather of one batch is in
+            # flight while the next batch is written into a second record set
+            parts, work = gather_records(rec.stage(), cap, rank, world, async_op=True)
+            rec2 = alloc_records(cap, "cpu")
+            rec2.buf.copy_(rec.buf)
+            rec2.out.copy_(rec.out)
+            parts2, work2 = gather_records(rec2.stage(), cap, rank, world, async_op=True)
+            work2.wait()
+            work.wait()
+            if rank == 0:
+                for a, b2 in zip(parts, parts2):
+                    assert torch.equal(a, b2)
+        else:
+            parts = gather_records(rec.stage(), cap, rank, world)
         if rank == 0:
             q.put(unpack_gathered(parts, T, world))
         else:
@@ -61,15 +75,15 @@ def _worker(rank, world, port, T, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,T", [(2, 37), (3, 20), (2, 1)])
-def test_gloo_shard_and_gather_reproduce_single_process(world, T):
+@pytest.mark.parametrize("world,T,async_op", [(2, 37, False), (3, 20, False), (2, 1, False), (2, 37, True)])
+def test_gloo_shard_and_gather_reproduce_single_process(world, T, async_op):
     from metadamage_amd.synthetic import generate
     from oracle.oracle import OracleLib
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, T, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, T, q, async_op)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)
