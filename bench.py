@@ -68,15 +68,16 @@ def parse():
     return a
 
 
-def pmc_traffic():
-    """Per-launch HBM bytes of fit_kernel from the committed rocprofv3 PMC
-    summary (profiles/pmc_fit_kernel.json), or None."""
-    f = ROOT / "profiles" / "pmc_fit_kernel.json"
+def pmc_traffic(kernel: str = "fit_kernel", taxa: int = TAXA_PER_GPU):
+    """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC
+    summary (profiles/pmc_<kernel>.json) when it was measured at this batch
+    size, else None."""
+    f = ROOT / "profiles" / f"pmc_{kernel}.json"
     if not f.exists():
         return None
     try:
         d = json.loads(f.read_text())
-        return d.get("hbm_bytes_per_launch")
+        return d.get("hbm_bytes_per_launch") if d.get("taxa_per_launch") == taxa else None
     except Exception:
         return None
 
@@ -182,7 +183,7 @@ def main():
         k_avg_s = fit_ms_sum / n_calls / 1e3
         call_avg_s = call_ms_sum / n_calls / 1e3
         achieved = FIT_BYTES_PER_TAXON * T / k_avg_s / 1e9
-        traffic = pmc_traffic()
+        traffic = pmc_traffic("fit_kernel", T)
         # compute roofline: register-only probe of the same point evaluation
         n_waves, iters = 256 * 16, 64
         engine.peak_probe(n_waves, iters, stream=stream)  # warm
@@ -287,7 +288,7 @@ def nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, 
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": pmc_traffic("nuts_chain_kernel", T),
             "kernel": "nuts_chain_kernel",
             "kernel_ms_avg": round(k_avg_s * 1e3, 3),
             "bytes_per_taxon": bytes_per_taxon,

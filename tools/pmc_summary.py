@@ -19,6 +19,8 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 TAXA = 10_000
 FIT_BYTES_PER_TAXON = 240 + 192 + 384  # bench.py
+NUTS_TAXA = 100_000
+NUTS_BYTES_PER_TAXON = 240 + 6 * 1000 * 32 + 6 * 32  # bench.py nuts_line
 
 
 def rows(path: Path):
@@ -53,25 +55,38 @@ def main() -> None:
     for name in ("bench_trace.json", "bench_nuts_trace.json"):
         if (src / name).exists():
             shutil.copy(src / name, prof / f"{tag}_{name}")
-    k = "mdfit::fit_kernel"
-    fetch_kb = counter_mean(found["pmc_fetch_size.csv"], k, "FETCH_SIZE")
-    write_kb = counter_mean(found["pmc_write_size.csv"], k, "WRITE_SIZE")
+    write_summary(prof, tag, "fit_kernel", TAXA, FIT_BYTES_PER_TAXON, found["kernel_stats.csv"],
+                  found["pmc_fetch_size.csv"], found["pmc_write_size.csv"], "python bench.py")
+    # the NUTS chain kernel at config C3 (optional passes)
+    nf, nw = sorted((src / "nuts_fetch").rglob("*counter_collection.csv")), sorted((src / "nuts_write").rglob("*counter_collection.csv"))
+    if nuts and nf and nw:
+        shutil.copy(nf[0], prof / f"{tag}_nuts_pmc_fetch_size.csv")
+        shutil.copy(nw[0], prof / f"{tag}_nuts_pmc_write_size.csv")
+        write_summary(prof, tag, "nuts_chain_kernel", NUTS_TAXA, NUTS_BYTES_PER_TAXON,
+                      prof / f"{tag}_nuts_kernel_stats.csv", prof / f"{tag}_nuts_pmc_fetch_size.csv",
+                      prof / f"{tag}_nuts_pmc_write_size.csv", "python bench.py --mode nuts")
+
+
+def write_summary(prof, tag, name, taxa, bytes_per_taxon, stats_csv, fetch_csv, write_csv, cmd):
+    k = f"mdfit::{name}" if name == "fit_kernel" else f"mdfit::nuts::{name}"
+    fetch_kb = counter_mean(fetch_csv, k, "FETCH_SIZE")
+    write_kb = counter_mean(write_csv, k, "WRITE_SIZE")
     # kernel names as rocprofv3 prints them: "void mdfit::fit_kernel<1>(...)"
-    fk = next((r for r in rows(found["kernel_stats.csv"]) if k in r["Name"].split("(")[0]), {})
+    fk = next((r for r in rows(stats_csv) if k in r["Name"].split("(")[0]), {})
     summary = {
         "kernel": k,
-        "taxa_per_launch": TAXA,
+        "taxa_per_launch": taxa,
         "FETCH_SIZE_kB_mean": fetch_kb,
         "WRITE_SIZE_kB_mean": write_kb,
         "correction": "gfx950: FETCH_SIZE x2 (MI355X_MICROARCH.md §HBM: FETCH_SIZE reports 1/2 of wide coalesced "
         "reads; this kernel's 4-B/lane and broadcast 8-B loads are uncalibrated), WRITE_SIZE x1",
         "hbm_bytes_per_launch": int(round((2 * fetch_kb + write_kb) * 1024)),
-        "algorithmic_bytes_per_launch": FIT_BYTES_PER_TAXON * TAXA,
+        "algorithmic_bytes_per_launch": bytes_per_taxon * taxa,
         "rocprof_avg_ns": float(fk.get("AverageNs", "nan")),
         "source": f"rocprofv3 --kernel-trace --stats; --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes; "
-        f"python bench.py (profiles/{tag}_*.csv)",
+        f"{cmd} (profiles/{tag}_*.csv)",
     }
-    (prof / "pmc_fit_kernel.json").write_text(json.dumps(summary, indent=1) + "\n")
+    (prof / f"pmc_{name}.json").write_text(json.dumps(summary, indent=1) + "\n")
     print(json.dumps(summary, indent=1))
 
 
