@@ -76,8 +76,11 @@ __device__ __forceinline__ int kpos(int i) { return i < kNHalf ? i : i - kNHalf;
 // by its own mode when it converged -- the warm start).
 __global__ __launch_bounds__(256) void init_kernel(const uint32_t* __restrict__ gy,
                                                    const uint32_t* __restrict__ gN, int64_t T,
-                                                   double* __restrict__ out) {
+                                                   double* __restrict__ out, int* __restrict__ ws) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // the fit kernel's queue counters (workspace, 256 B): zeroed here instead of
+  // by a separate memset launch (stream order puts this before the fit kernel)
+  if (i < 64) ws[i] = 0;
   if (i >= MDFIT_NSUBFIT * T) return;
   const int64_t taxon = i / MDFIT_NSUBFIT;
   const int sub = (int)(i % MDFIT_NSUBFIT);  // 0 PMD-all 1 null-all 2 PMD-f 3 PMD-r 4 null-f 5 null-r
@@ -877,10 +880,8 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   hipStream_t s = (hipStream_t)hip_stream;
   int* ws = (int*)workspace;
   prof_record(0, s);
-  if (hipMemsetAsync(ws, 0, 256, s) !=
-      hipSuccess)
-    return check_launch("hipMemsetAsync(workspace)");
   if (o.mode == MDFIT_MODE_NUTS) {
+    if (hipMemsetAsync(ws, 0, 256, s) != hipSuccess) return check_launch("hipMemsetAsync(workspace)");
     if (int rc = mdfit::nuts::fit_batch(y, N, mm, n_taxa, o, out, pred, status, workspace, s)) return rc;
     prof_record(3, s);
     if (g_prof.on && g_prof.n < kProfMax) ++g_prof.n;
@@ -888,7 +889,7 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   }
   const int64_t n_init = MDFIT_NSUBFIT * n_taxa;
   hipLaunchKernelGGL(mdfit::init_kernel, dim3((unsigned)((n_init + 255) / 256)), dim3(256), 0, s, y, N,
-                     n_taxa, out);
+                     n_taxa, out, ws);
   if (int rc = check_launch("init_kernel")) return rc;
   // lane layout of the fit kernel (bitwise-identical results): 2 points per
   // lane for batches that fill the chip several times over, 1 below (lower

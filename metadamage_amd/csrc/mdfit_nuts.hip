@@ -154,7 +154,8 @@ __device__ __forceinline__ Pot potential(const PointData& pd, const double v[4],
   const double phi = delta + 2.0;
   const bool pmd = pd.pmd;
   const double A = pmd ? A0 : 0.0, c = pmd ? c0 : 0.0;
-  double lprior = prq + v[3] - delta / 1000.0;
+  // Exponential(rate 1/1000).log_prob = log(rate) - rate * delta (numpyro's form)
+  double lprior = prq + v[3] - delta * 1e-3;
   if (pmd) lprior += prA + prc;
 
   double D, dq, dA;
@@ -195,7 +196,7 @@ __device__ __forceinline__ Pot potential(const PointData& pd, const double v[4],
   o.g[0] = -(acc[1] * (q * omq) + (2.0 - 5.0 * q));
   o.g[1] = pmd ? -(acc[2] * (A * omA) + (2.0 - 5.0 * A)) : 0.0;
   o.g[2] = pmd ? -(acc[3] * (c * omc) + (1.0 - 10.0 * c)) : 0.0;
-  o.g[3] = -(acc[4] * delta + (1.0 - delta / 1000.0));
+  o.g[3] = -(acc[4] * delta + (1.0 - delta * 1e-3));
   if (bad || !isfinite(o.U)) {
     o.U = INFINITY;
     o.g[0] = o.g[1] = o.g[2] = o.g[3] = 0.0;
@@ -293,6 +294,7 @@ struct ChainState {
   double pz[4], pr[4], pg[4];
   double step, eps, e0;
   double invm[4];
+  double isd[4];  // sqrt(1 / invm): the momentum scale, recomputed when invm changes
   // step-size search
   int f_call, f_m, f_last, f_dir;
   // dual averaging, windows
@@ -320,7 +322,7 @@ __device__ __forceinline__ void chain_init(ChainState& c) {
   c.it = c.attempt = 0;
   for (int j = 0; j < 4; ++j) {
     c.pz[j] = c.pr[j] = c.pg[j] = c.t_rsum[j] = c.s_rsum[j] = 0.0;
-    c.invm[j] = 1.0;
+    c.invm[j] = c.isd[j] = 1.0;
   }
   c.step = 0.0;
   c.eps = 1.0;
@@ -397,6 +399,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   double& eps = C.eps;
   double& e0 = C.e0;
   double* invm = C.invm;
+  double* isd = C.isd;
   int& f_call = C.f_call;
   int& f_m = C.f_m;
   int& f_last = C.f_last;
@@ -514,7 +517,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       for (int j = 0; j < 4; ++j) {
         pz[j] = active(pd.pmd, j) ? -2.0 + 4.0 * uniform(st, 0xFFFF0000u, (uint32_t)j) : 0.0;
         pr[j] = pg[j] = 0.0;
-        invm[j] = 1.0;
+        invm[j] = isd[j] = 1.0;
         R.wmean[j] = R.wm2[j] = 0.0;
       }
     }
@@ -618,7 +621,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         const double m = fmax(s_w, w);
         const double e = exp(-fabs(s_w - w));
         const double nw = m == -INFINITY ? -INFINITY : m + flog1p(e);
-        const double prob = (w >= s_w ? 1.0 : e) / (1.0 + e);
+        const double prob = (w >= s_w ? 1.0 : e) * rcp(1.0 + e);
         if ((leaf_ctr >> 4) != C.ul_chunk) {  // next 16 leaf uniforms, one per lane
           sul[lane] = uniform(st, (uint32_t)it, 32u + (uint32_t)(leaf_ctr & ~15) + (uint32_t)i);
           C.ul_chunk = leaf_ctr >> 4;
@@ -737,6 +740,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
                 if (!active(pd.pmd, j)) continue;
                 const double var = R.wm2[j] / (wn - 1);
                 invm[j] = ((double)wn / (wn + 5.0)) * var + 1e-3 * (5.0 / (wn + 5.0));
+                isd[j] = sqrt(1.0 / invm[j]);
                 R.wmean[j] = R.wm2[j] = 0.0;
               }
               wn = 0;
@@ -798,7 +802,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       row4(normal(st, 0xFFFE0000u + 4096u * (uint32_t)f_call + (uint32_t)f_m, (uint32_t)(i & 3)), nj);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        pr[j] = active(pd.pmd, j) ? nj[j] * sqrt(1.0 / invm[j]) : 0.0;
+        pr[j] = active(pd.pmd, j) ? nj[j] * isd[j] : 0.0;
         pz[j] = R.tz[j];
         pg[j] = R.tg[j];
       }
@@ -811,7 +815,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       row4(normal(st, (uint32_t)it, (uint32_t)(i & 3)), nj);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        pr[j] = active(pd.pmd, j) ? nj[j] * sqrt(1.0 / invm[j]) : 0.0;
+        pr[j] = active(pd.pmd, j) ? nj[j] * isd[j] : 0.0;
         pz[j] = R.tz[j];
         pg[j] = R.tg[j];
         R.lz[j] = R.rz[j] = pz[j];

@@ -153,8 +153,9 @@ static double nuts_potential(int model, const uint32_t* y, const uint32_t* N, in
   }
   /* log prior + log|J|: q, A ~ Beta(2,3) -> 2 ln p + 3 ln(1-p); c ~ Beta(1,9)
    * -> ln c + 9 ln(1-c); delta ~ Exp(1/1000) -> v3 - delta/1000 */
-  double lp = 2.0 * lq + 3.0 * l1q + v[3] - delta / 1000.0;
-  double gq = 2.0 - 5.0 * q, gA = 0, gc = 0, gd = 1.0 - delta / 1000.0;
+  /* Exponential(rate 1/1000).log_prob = log(rate) - rate * delta (numpyro's form) */
+  double lp = 2.0 * lq + 3.0 * l1q + v[3] - delta * 1e-3;
+  double gq = 2.0 - 5.0 * q, gA = 0, gc = 0, gd = 1.0 - delta * 1e-3;
   if (model == M_PMD) {
     lp += 2.0 * lA + 3.0 * l1A + lc + 9.0 * l1c;
     gA = 2.0 - 5.0 * A;
