@@ -304,7 +304,8 @@ struct ChainState {
   double t_w, t_rsum[4], t_acc, u_tr;
   int t_n, t_depth, leaf_ctr, nleap;
   bool t_turn, t_div, right;
-  // subtree
+  // subtree (the kernel keeps s_w .. nmax and leaf_ctr in registers; the
+  // fields stay: removing them measurably changes the register allocation)
   double s_w, s_rsum[4], s_acc;
   int s_n, n_leaf, nmax;
   bool s_div;
@@ -416,17 +417,16 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   double& u_tr = C.u_tr;
   int& t_n = C.t_n;
   int& t_depth = C.t_depth;
-  int& leaf_ctr = C.leaf_ctr;
+  int leaf_ctr = 0;
   int& nleap = C.nleap;
   bool& t_turn = C.t_turn;
   bool& t_div = C.t_div;
   bool& right = C.right;
-  double& s_w = C.s_w;
-  double* s_rsum = C.s_rsum;
-  double& s_acc = C.s_acc;
-  int& s_n = C.s_n;
-  int& n_leaf = C.n_leaf;
-  int& nmax = C.nmax;
+  int& ul_chunk = C.ul_chunk;
+  // the subtree being built: touched by every leaf, so kept in registers
+  // (row-uniform like the LDS state; A/B: -3.5 % chain time at C3)
+  double s_w = 0.0, s_rsum[4] = {0, 0, 0, 0}, s_acc = 0.0;
+  int s_n = 0, n_leaf = 0, nmax = 1;
   bool& s_div = C.s_div;
   double& st_div = C.st_div;
   double& st_leap = C.st_leap;
@@ -444,10 +444,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   }
   __syncthreads();
 #ifdef MDFIT_STAMP
-  // [0] top, [1] after the task start, [2] after the potential, [3] after the
-  // mode dispatch, [4] end of the body; acc: start, potential, dispatch, begin, trips
-  __shared__ unsigned long long sstamp[5];
-  unsigned long long acc_t[5] = {0, 0, 0, 0, 0};
+  // stamp k (set by whichever lanes reach point k; 0 = not reached this trip)
+  // opens section k: 0 task start, 1 potential, 2 mode dispatch up to the leaf
+  // weights, 5 checkpoints + U-turn checks, 6 subtree merge, 7 transition end
+  // (adaptation / draw), 8 rest of the dispatch, 3 begin probe / iteration,
+  // 4 loop tail.  acc_t[k]: cycles per section, acc_t[9]: trips
+  constexpr int kNStamp = 10;
+  __shared__ unsigned long long sstamp[kNStamp];
+  unsigned long long acc_t[kNStamp] = {};
   const unsigned long long t_begin = nstamp();
   sstamp[0] = 0;
 #endif
@@ -456,18 +460,22 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
 #ifdef MDFIT_STAMP
     {
       const unsigned long long now = nstamp();
-      if (sstamp[0] != 0) {  // book the previous trip
-        const unsigned long long t3 = sstamp[3] ? sstamp[3] : now, t4 = sstamp[4] ? sstamp[4] : now;
-        const unsigned long long t2 = sstamp[2] ? sstamp[2] : t3;
-        const unsigned long long t1 = sstamp[1] ? sstamp[1] : t2;
-        acc_t[0] += t1 - sstamp[0];
-        acc_t[1] += t2 - t1;
-        acc_t[2] += t3 - t2;
-        acc_t[3] += now - t3;
-        acc_t[4] += 1;
+      if (sstamp[0] != 0) {  // book the previous trip, sections in program order
+        constexpr int order[9] = {0, 1, 2, 5, 6, 7, 8, 3, 4};
+        int cur = 0;
+        unsigned long long last = sstamp[0];
+        for (int j = 1; j < 9; ++j) {
+          const int k = order[j];
+          if (sstamp[k] == 0) continue;
+          acc_t[cur] += sstamp[k] - last;
+          last = sstamp[k];
+          cur = k;
+        }
+        acc_t[cur] += now - last;
+        acc_t[9] += 1;
       }
       sstamp[0] = now;
-      sstamp[1] = sstamp[2] = sstamp[3] = sstamp[4] = 0;
+      for (int j = 1; j < kNStamp; ++j) sstamp[j] = 0;
     }
 #endif
     // ---- 1. free groups start a task (one atomic per wave-trip) --------------
@@ -622,9 +630,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         const double e = exp(-fabs(s_w - w));
         const double nw = m == -INFINITY ? -INFINITY : m + flog1p(e);
         const double prob = (w >= s_w ? 1.0 : e) * rcp(1.0 + e);
-        if ((leaf_ctr >> 4) != C.ul_chunk) {  // next 16 leaf uniforms, one per lane
+        if ((leaf_ctr >> 4) != ul_chunk) {  // next 16 leaf uniforms, one per lane
           sul[lane] = uniform(st, (uint32_t)it, 32u + (uint32_t)(leaf_ctr & ~15) + (uint32_t)i);
-          C.ul_chunk = leaf_ctr >> 4;
+          ul_chunk = leaf_ctr >> 4;
         }
         if (sul[row16 + (leaf_ctr & 15)] < prob) {
 #pragma unroll
@@ -640,6 +648,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         s_acc += acc;
         s_n += 1;
       }
+      NSTAMP(5);
       s_div = dv;
       ++leaf_ctr;
       int imin, imax;
@@ -668,6 +677,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       for (int j = 0; j < 4; ++j) pr[j] = rn[j];
 #pragma unroll
       for (int j = 0; j < 4; ++j) pg[j] = P.g[j];
+      NSTAMP(6);
       if (s_turn || s_div || n_leaf == nmax) {
         // merge the subtree into the tree: biased progressive sampling
         // prob = min(1, exp(s_w - t_w)) and t_w' = logaddexp(t_w, s_w) from one
@@ -708,6 +718,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         t_n += s_n;
         ++t_depth;
         if (t_depth >= kMaxDepth || t_turn || t_div) {
+          NSTAMP(7);
           // ---- the transition is complete: adapt or keep the draw ----------
           const double accp = t_acc / (double)t_n;
           if (it < W) {
@@ -768,6 +779,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
           } else if (!begin_find) {
             begin_iter = true;
           }
+          NSTAMP(8);
         } else {
           // next doubling
           const int j = t_depth;
@@ -834,7 +846,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       // this iteration's doubling draws, lane j of the row for depth j
       sdb[lane] = (int)(block(st, (uint32_t)it, 4u + 2u * (uint32_t)i).x & 1u);
       sut[lane] = uniform(st, (uint32_t)it, 5u + 2u * (uint32_t)i);
-      C.ul_chunk = -1;
+      ul_chunk = -1;
       right = sdb[row16] != 0;
       u_tr = sut[row16];
       n_leaf = 0;
@@ -845,9 +857,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   }
 #ifdef MDFIT_STAMP
   if (lane == 0 && g_nuts_stamp) {
-    unsigned long long* w = g_nuts_stamp + 8 * (size_t)blockIdx.x;
-    for (int j = 0; j < 5; ++j) w[j] = acc_t[j];
-    w[5] = nstamp() - t_begin;
+    unsigned long long* w = g_nuts_stamp + 16 * (size_t)blockIdx.x;
+    for (int j = 0; j < kNStamp; ++j) w[j] = acc_t[j];
+    w[10] = nstamp() - t_begin;
   }
 #endif
 }
