@@ -1017,7 +1017,11 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
   __shared__ double s_rec[MDFIT_NOUT];
   __shared__ double s_tmp[kWave];
   __shared__ double s_waic[MDFIT_NSUBFIT][kNPos];
-  __shared__ double s_v[kMaxSamples];
+  // the per-draw values (pointwise log-likelihoods, predictive fractions): the
+  // launch sizes it to the sort's power of two >= S (8 KB at S = 1000; a
+  // fixed kMaxSamples array made the block 37 KB and capped the kernel at one
+  // wave per SIMD)
+  extern __shared__ double s_v[];
   const int lane = threadIdx.x;
   const int64_t t = blockIdx.x;
   const int S = o.num_samples;
@@ -1246,8 +1250,10 @@ int fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t 
   hipLaunchKernelGGL(nuts_chain_kernel, dim3((unsigned)g), dim3(kWave), 0, s, y, N, n_taxa, o, out, ws, samples);
   if (int rc = host::check_launch("nuts_chain_kernel")) return rc;
   host::prof_mark(2, s);
-  hipLaunchKernelGGL(nuts_post_kernel, dim3((unsigned)n_taxa), dim3(kWave), 0, s, y, N, mm, n_taxa, o, samples, out,
-                     pred, status);
+  size_t sv_bytes = sizeof(double);
+  while (sv_bytes < (size_t)o.num_samples * sizeof(double)) sv_bytes <<= 1;  // lds_sort pads to 2^k
+  hipLaunchKernelGGL(nuts_post_kernel, dim3((unsigned)n_taxa), dim3(kWave), sv_bytes, s, y, N, mm, n_taxa, o,
+                     samples, out, pred, status);
   return host::check_launch("nuts_post_kernel");
 }
 
