@@ -194,7 +194,8 @@ int mdfit_nuts_potential(const int32_t* model, const int32_t* subset, const uint
 
 /* Profiling hooks (bench / roofline): while enabled, every mdfit_fit_batch
  * records HIP events on its stream around the whole call and around the fit
- * kernel (up to 256 calls).  mdfit_profile_read synchronises on them and
+ * kernel (up to 256 calls); on = 2 records only the two events around the fit
+ * kernel (call_ms then reads -1).  mdfit_profile_read synchronises on them and
  * returns the summed milliseconds and the number of calls, then resets. */
 int mdfit_profile_enable(int on);
 int mdfit_profile_read(double* call_ms, double* fit_ms, int32_t* n_calls);

@@ -797,6 +797,7 @@ constexpr int kProfMax = 256;
 constexpr int64_t kPpl2MinTaxa = 30000;  // measured crossover: 25-30k taxa
 struct ProfState {
   bool on = false;
+  bool fit_only = false;  // mdfit_profile_enable(2): only the events around fit_kernel
   int n = 0;
   hipEvent_t ev[kProfMax][4];
   bool made = false;
@@ -804,6 +805,7 @@ struct ProfState {
 ProfState g_prof;
 
 void prof_record(int slot, hipStream_t s) {
+  if (g_prof.fit_only && (slot == 0 || slot == 3)) return;
   if (g_prof.on && g_prof.n < kProfMax) (void)hipEventRecord(g_prof.ev[g_prof.n][slot], s);
 }
 }  // namespace
@@ -820,6 +822,7 @@ int mdfit_profile_enable(int on) {
     g_prof.made = true;
   }
   g_prof.on = on != 0;
+  g_prof.fit_only = on == 2;
   g_prof.n = 0;
   return 0;
 }
@@ -829,14 +832,15 @@ int mdfit_profile_read(double* call_ms, double* fit_ms, int32_t* n_calls) {
   double a = 0.0, b = 0.0;
   for (int i = 0; i < g_prof.n; ++i) {
     float x = 0.f, y = 0.f;
-    if (hipEventSynchronize(g_prof.ev[i][3]) != hipSuccess ||
-        hipEventElapsedTime(&x, g_prof.ev[i][0], g_prof.ev[i][3]) != hipSuccess ||
+    if (hipEventSynchronize(g_prof.ev[i][2]) != hipSuccess ||
+        (!g_prof.fit_only && (hipEventSynchronize(g_prof.ev[i][3]) != hipSuccess ||
+                              hipEventElapsedTime(&x, g_prof.ev[i][0], g_prof.ev[i][3]) != hipSuccess)) ||
         hipEventElapsedTime(&y, g_prof.ev[i][1], g_prof.ev[i][2]) != hipSuccess)
       return set_err(MDFIT_E_HIP, "hipEventElapsedTime");
     a += x;
     b += y;
   }
-  *call_ms = a;
+  *call_ms = g_prof.fit_only ? -1.0 : a;  // not recorded in fit-only mode
   *fit_ms = b;
   *n_calls = g_prof.n;
   g_prof.n = 0;

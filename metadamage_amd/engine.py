@@ -185,10 +185,11 @@ def nuts_potential(model, subset, y, N, v, device="cuda"):
     return U.cpu().numpy(), g.cpu().numpy()
 
 
-def profile_enable(on: bool = True) -> None:
+def profile_enable(on: bool = True, fit_only: bool = False) -> None:
     """Record HIP events around every following mdfit_fit_batch call (and its
-    fit kernel) on the call's stream."""
-    _lib.check(_lib.load().mdfit_profile_enable(1 if on else 0))
+    fit kernel) on the call's stream; fit_only: only the two around the fit
+    kernel (profile_read's call time is then -1)."""
+    _lib.check(_lib.load().mdfit_profile_enable((2 if fit_only else 1) if on else 0))
 
 
 def profile_read():
