@@ -464,14 +464,22 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         constexpr int order[9] = {0, 1, 2, 5, 6, 7, 8, 3, 4};
         int cur = 0;
         unsigned long long last = sstamp[0];
+        // (acc_t indexed by literals only: a runtime index would put it in
+        // scratch and charge global-memory round trips to the task start)
+#pragma unroll
         for (int j = 1; j < 9; ++j) {
           const int k = order[j];
           if (sstamp[k] == 0) continue;
-          acc_t[cur] += sstamp[k] - last;
+          const unsigned long long d = sstamp[k] - last;
+#pragma unroll
+          for (int q = 0; q < 9; ++q)
+            if (q == cur) acc_t[q] += d;
           last = sstamp[k];
           cur = k;
         }
-        acc_t[cur] += now - last;
+#pragma unroll
+        for (int q = 0; q < 9; ++q)
+          if (q == cur) acc_t[q] += now - last;
         acc_t[9] += 1;
       }
       sstamp[0] = now;
