@@ -226,6 +226,8 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "kernel": "fit_kernel",
+                "note": "HBM fraction is structural (816 B per taxon against ~1e3 FP64 point evaluations); "
+                "the kernel is FP64-VALU / latency bound: see compute_roofline (SURVEY.md 8(d), DESIGN.md 4)",
                 "kernel_ms_avg": round(k_avg_s * 1e3, 4),
                 "bytes_per_taxon": FIT_BYTES_PER_TAXON,
                 "call_ms_avg": round(call_avg_s * 1e3, 4),
@@ -293,6 +295,8 @@ def nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, 
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": pmc_traffic("nuts_chain_kernel", T),
             "kernel": "nuts_chain_kernel",
+            "note": "HBM fraction is structural (the draws written, 192 KB per taxon, against ~2e6 leapfrog "
+            "point evaluations); the kernel is FP64-VALU / latency bound (DESIGN.md 9)",
             "kernel_ms_avg": round(k_avg_s * 1e3, 3),
             "bytes_per_taxon": bytes_per_taxon,
             "call_ms_avg": round(call_ms_sum / n_calls, 3),
