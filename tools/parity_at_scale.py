@@ -1,0 +1,51 @@
+"""MAP parity at full BASELINE sizes (evidence for DESIGN.md §5): the HIP fit of
+C2 (10k taxa, seed 1), C3's size (100k, seed 2) and C4's per-GPU share (125k,
+seed 3) against the CPU oracle on all 25 result columns, with bench.py's
+metric (|gpu - cpu| / max(|cpu|, 1e-2) over taxa both fitted) and the status
+agreement, as one JSON line per size.
+
+    python tools/parity_at_scale.py > profiles/r01_parity_at_scale.jsonl
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def main() -> None:
+    import torch
+
+    from bench import parity
+    from metadamage_amd import engine
+    from metadamage_amd.synthetic import generate
+    from oracle.oracle import OracleLib
+
+    oracle = OracleLib()
+    threads = min(16, os.cpu_count() or 1)
+    for T, seed, label in ((10_000, 1, "C2"), (100_000, 2, "C3 size, MAP"), (125_000, 3, "C4 per-GPU share")):
+        b = generate(T, seed=seed)
+        out, pred, st = engine.fit_batch(b.y, b.N, b.mm)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ref, rpred, rst = oracle.fit_batch(b.y, b.N, b.mm, threads=threads)
+        cpu_s = time.perf_counter() - t0
+        line = parity(out, st, ref, rst, kind="MAP, same MDFIT-MAP v1 as the oracle")
+        line.update(config=label, n_taxa=T, seed=seed, gpu_status_ok=float((st == 0).mean()),
+                    cpu_status_ok=float((rst == 0).mean()),
+                    status_mismatch_tax_index=[int(i) for i in np.nonzero(st != rst)[0][:10]],
+                    pred_max_abs=float(np.nanmax(np.abs(pred - rpred))), oracle_s=round(cpu_s, 2),
+                    oracle_threads=threads)
+        print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
