@@ -149,6 +149,8 @@ int64_t mdfit_workspace_bytes(int64_t n_taxa, const mdfit_opts* opts);
  * fits.py:59,67 and log_likelihood fits.py:126-133):
  *   out[i] = log C(N,y) + lnB(y+alpha, N-y+beta) - lnB(alpha, beta)
  * plus d/dalpha, d/dbeta (grad[i][2]).  Device pointers; for parity tests.
+ * The value is computed in the cancellation-free form the record assembly
+ * uses for its pointwise log-likelihoods (rising-factorial ratios).
  */
 int mdfit_betabinom_logpmf(const double* y, const double* N, const double* alpha,
                            const double* beta, int64_t n, double* out,
@@ -164,7 +166,8 @@ int mdfit_special(const double* x, int64_t n, double* out3, void* hip_stream);
  * Objective of one sub-fit at given unconstrained parameters, evaluated by
  * the fit kernel's own lane layout and code (parity tests).  Per item i:
  * model[i] (0 PMD, 1 null), subset[i] (0 all, 1 forward, 2 reverse),
- * y/N rows [n][MDFIT_LD], u[n][4] = (logit q, logit A, logit c, log delta).
+ * y/N rows [n][MDFIT_LD], u[n][4] = (logit q, logit A, c, log delta) -- c on
+ * its own scale (MDFIT-MAP v1; the sampler uses logit c).
  * Outputs F[n] = -(sum ell + log prior), g[n][4], H[n][4][4] (d/du),
  * ell[n][30] (pointwise log-lik without log C(N,y); 0 outside the subset).
  */

@@ -662,11 +662,11 @@ __global__ void betabinom_kernel(const double* __restrict__ y, const double* __r
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const double k = y[i], m = N[i], al = a[i], be = b[i];
-  const LG3 c0 = lg3(m + 1.0), c1 = lg3(k + 1.0), c2 = lg3(m - k + 1.0);
-  const LG3 t1 = lg3(k + al), t2 = lg3(m - k + be), t3 = lg3(m + al + be);
-  const LG3 t4 = lg3(al), t5 = lg3(be), t6 = lg3(al + be);
-  o[i] = (c0.l - c1.l - c2.l) + (t1.l + t2.l - t3.l) - (t4.l + t5.l - t6.l);
+  // value: the cancellation-free form the record assembly uses (bb_logpmf)
+  o[i] = bb_logpmf_ab(k, m, al, be, al + be);
   if (g != nullptr) {
+    const LG3 t1 = lg3(k + al), t2 = lg3(m - k + be), t3 = lg3(m + al + be);
+    const LG3 t4 = lg3(al), t5 = lg3(be), t6 = lg3(al + be);
     const double ps = t6.p - t3.p;
     g[2 * i + 0] = t1.p - t4.p + ps;
     g[2 * i + 1] = t2.p - t5.p + ps;

@@ -261,14 +261,14 @@ __device__ __forceinline__ double point_accum(const PointData& pd, const Theta& 
   return point_contrib(pd, th, t3, t6, acc);
 }
 
-// Value-only log-likelihood of one point (lnGamma only; the record assembly
-// needs the pointwise log-likelihoods at the modes).
+// Pointwise log-likelihood of one point at a mode for the record assembly
+// (waic_i = -2 ell_i, fits.py:126-172): the full log-pmf including log C(N,y)
+// -- what numpyro's log_likelihood returns -- in the cancellation-free form
+// bb_logpmf.  (The fit objective drops the data-only log C(N,y); it cancels in
+// n_sigma / asymmetry, but without it ell_i is ~ -N H(y/N) ~ 1e8 and a 1-ulp
+// lnGamma difference becomes ~1e-4 of a small WAIC-difference statistic.)
 __device__ __forceinline__ double point_ell(double y, double N, double D, double phi) {
-  const double a = D * phi, b = (1.0 - D) * phi;
-  const double la = lg3(y + a).l - lg3(a).l;
-  const double lb = lg3(N - y + b).l - lg3(b).l;
-  const double lS = lg3(N + phi).l - lg3(phi).l;
-  return (la + lb) - lS;
+  return bb_logpmf(y, N, D, phi);
 }
 
 // Objective in u-space from the group sums (oracle: evaluate(), chain rule

@@ -128,4 +128,60 @@ __device__ __forceinline__ LG3 lg3(double x) {
   return {L, Ps, Q};
 }
 
+// lnGamma alone (the unused psi is dead code after inlining)
+__device__ __forceinline__ double lgam(double x) { return lg3<false>(x).l; }
+
+// Stirling remainder lnGamma(z) - [(z - 1/2) ln z - z + ln(2 pi)/2], z >= 10
+// (the series of lg3, O(z^-15))
+__device__ __forceinline__ double stirling_rem(double z) {
+  const double r = rcp(z), r2 = r * r;
+  double sl = fma(r2, -1.0 / 156.0, 691.0 / 360360.0);
+  sl = fma(r2, -sl, 1.0 / 1188.0);
+  sl = fma(r2, -sl, 1.0 / 1680.0);
+  sl = fma(r2, -sl, 1.0 / 1260.0);
+  sl = fma(r2, -sl, 1.0 / 360.0);
+  sl = fma(r2, -sl, 1.0 / 12.0);
+  return r * sl;
+}
+
+// lnGamma(z + h) - lnGamma(z) for z, z + h > 0, without subtracting two large
+// lnGamma values and without rounding the argument z + h (at z ~ 2e9 one ulp
+// of it moves lnGamma by ~5e-6): in the Stirling range the leading terms are
+// differenced analytically,
+//   (z+h-1/2) ln(z+h) - (z+h) - (z-1/2) ln z + z = (z - 1/2 + h) log1p(h/z) + h (ln z - 1),
+// so the rounding error scales with the difference, not with lnGamma ~ z ln z
+// (one ulp of lnGamma(1e9) is ~4e-6); the remainders' difference is tiny.
+// Below 10 the plain difference (small values, nothing to cancel).
+__device__ __forceinline__ double lgdiff(double z, double h) {
+  const double z1 = z + h;  // only for the branch test and the remainder
+  if (z >= 10.0 && z1 >= 10.0) {
+    const double t = flog1p(h * rcp(z));
+    return fma(z - 0.5 + h, t, h * (flog(z) - 1.0)) + (stirling_rem(z1) - stirling_rem(z));
+  }
+  return lgam(z1) - lgam(z);
+}
+
+// ln[ Gamma(n+s) / (Gamma(n+1) Gamma(s)) ] = ln((s)_n / n!) for a count n >= 0
+// and s > 0: the large lnGamma of the bigger of (n+1, s) is differenced
+// against lnGamma(n+s) (lgdiff, with an exact step: s - 1 or the count n) and
+// only the smaller one's lnGamma is subtracted, so the result carries
+// rounding of the size of its own terms.
+__device__ __forceinline__ double lrise(double n, double s) {
+  if (n == 0.0) return 0.0;
+  return s <= n + 1.0 ? lgdiff(n + 1.0, s - 1.0) - lgam(s) : lgdiff(s, n) - lgam(n + 1.0);
+}
+
+// Full beta-binomial log-pmf (numpyro BetaBinomial.log_prob with log C(N,y),
+// fits.py:59,67,126-133) of one point at (D, phi):
+//   log C(N,y) + lnB(y+a, N-y+b) - lnB(a, b) = R(y,a) + R(N-y,b) - R(N,phi),
+// R = lrise, a = D phi, b = (1-D) phi.  Each R is O(s ln(n/s)), so the
+// O(10)-sized result keeps ~1e-11 absolute accuracy even at N ~ 4e9, where the
+// unnormalised form (a sum of lnGamma values ~1e11) would carry ~1e-5.
+__device__ __forceinline__ double bb_logpmf_ab(double y, double N, double a, double b, double phi) {
+  return (lrise(y, a) + lrise(N - y, b)) - lrise(N, phi);
+}
+__device__ __forceinline__ double bb_logpmf(double y, double N, double D, double phi) {
+  return bb_logpmf_ab(y, N, D * phi, (1.0 - D) * phi, phi);
+}
+
 }  // namespace mdfit

@@ -465,6 +465,66 @@ done:
   out->status = status;
 }
 
+/* ---- pointwise log-likelihood at a mode (fits.py:126-133) -----------------
+ * The record's WAIC statistics use the full beta-binomial log-pmf (numpyro's
+ * log_likelihood, log C(N,y) included), computed in long double as
+ *   R(y, a) + R(N-y, b) - R(N, phi),  R(n, s) = lnG(n+s) - lnG(n+1) - lnG(s),
+ * where each R is formed without subtracting two large lnGamma values and
+ * without rounding a sum like n + s (at n ~ 2e9 one ulp of the argument moves
+ * lnGamma by ~5e-6): lnG(z + h) - lnG(z) for z, z + h >= 8 is the difference
+ * of the Stirling expansions taken term by term -- the leading terms as
+ * (z - 1/2 + h) log1p(h/z) + h (ln z - 1), then the Bernoulli series
+ * B_2k/(2k(2k-1) x^(2k-1)) to k = 9.  The plain sum of lnGamma values (~1e11
+ * at N = 4e9) would carry ~1e-5 absolute error into an O(10) result.
+ * (Restated from the math, not from the kernel; the kernel's bb_logpmf is
+ * the same decomposition in double.)  Checked against mpmath at 40 digits
+ * (tests/test_oracle_golden.py). */
+static long double lgdiff_l(long double z, long double h) {
+  if (z >= 8.0L && z + h >= 8.0L) {
+    static const long double bern[9] = {1.0L / 12, -1.0L / 360, 1.0L / 1260, -1.0L / 1680, 1.0L / 1188,
+                                        -691.0L / 360360, 1.0L / 156, -3617.0L / 122400,
+                                        43867.0L / 244188};
+    long double t = log1pl(h / z);
+    long double s = (z - 0.5L + h) * t + h * (logl(z) - 1.0L);
+    long double r1 = 1.0L / (z + h), r2 = 1.0L / z, p1 = r1, p2 = r2;
+    for (int k = 0; k < 9; k++) {
+      s += bern[k] * (p1 - p2);
+      p1 *= r1 * r1;
+      p2 *= r2 * r2;
+    }
+    return s;
+  }
+  return lgammal(z + h) - lgammal(z);
+}
+
+static long double lrise_l(long double n, long double s) {
+  if (n == 0.0L) return 0.0L;
+  return s <= n + 1.0L ? lgdiff_l(n + 1.0L, s - 1.0L) - lgammal(s) : lgdiff_l(s, n) - lgammal(n + 1.0L);
+}
+
+static double bb_logpmf_full(double y, double N, double D, double phi) {
+  long double a = (long double)D * phi, b = (1.0L - (long double)D) * phi;
+  return (double)(lrise_l(y, a) + lrise_l(N - y, b) - lrise_l(N, phi));
+}
+
+/* the full pointwise log-pmf of sub-fit points [lo, hi) at its mode u */
+static void mode_ell(int model, const uint32_t* y, const uint32_t* N, int lo, int hi,
+                     const double u[4], double* ell) {
+  double q = sigm(u[P_Q]), phi = exp(u[P_D]) + 2.0;
+  double A = model == M_PMD ? sigm(u[P_A]) : 0.0, c = model == M_PMD ? u[P_C] : 0.0;
+  for (int i = lo; i < hi; i++) {
+    double D = model == M_PMD ? A * pow(1.0 - q, kpos(i)) + c : q;
+    ell[i] = bb_logpmf_full((double)y[i], (double)N[i], D, phi);
+  }
+}
+
+/* the same on arrays (alpha, beta given: phi = alpha + beta), for tests */
+void oracle_bb_logpmf_full(const double* y, const double* N, const double* a, const double* b, int64_t n,
+                           double* out) {
+  for (int64_t i = 0; i < n; i++)
+    out[i] = (double)(lrise_l(y[i], a[i]) + lrise_l(N[i] - y[i], b[i]) - lrise_l(N[i], (long double)(a[i] + b[i])));
+}
+
 /* n_sigma of fits.py:194-201 with one posterior "sample" (the mode):
  * lppd_i = ell_i, pWAIC_i = 0, waic_i = -2 ell_i (fits.py:147-172) */
 static double n_sigma(const double* lP, const double* lN, int n) {
@@ -611,7 +671,10 @@ static void fit_taxon(const uint32_t* y, const uint32_t* N, const uint32_t* mm,
       out[MDFIT_F_D_MAX_UPPER_HPDI] = p[2];
     }
   }
-  out[MDFIT_F_N_SIGMA] = n_sigma(f[0].r.ell, f[1].r.ell, NPOS);
+  /* pointwise full log-pmf of every sub-fit at its mode (the WAIC inputs) */
+  double ell[6][NPOS];
+  for (int s = 0; s < 6; s++) mode_ell(models[s], y, N, los[s], his[s], f[s].u, ell[s]);
+  out[MDFIT_F_N_SIGMA] = n_sigma(ell[0], ell[1], NPOS);
   out[MDFIT_F_Q_MEAN] = qa;
   out[MDFIT_F_CONCENTRATION_MEAN] = pa;
   out[MDFIT_F_D_MAX_MARGINALIZED_MEAN] = Aa + ca;
@@ -631,7 +694,7 @@ static void fit_taxon(const uint32_t* y, const uint32_t* N, const uint32_t* mm,
   out[MDFIT_F_Y_SUM_REVERSE] = yr;
   out[MDFIT_F_Y_SUM_TOTAL] = yf + yr;
   /* forward (fits.py:311-329) */
-  out[MDFIT_F_N_SIGMA_FORWARD] = n_sigma(f[2].r.ell, f[4].r.ell, NHALF);
+  out[MDFIT_F_N_SIGMA_FORWARD] = n_sigma(ell[2], ell[4], NHALF);
   {
     const double* dg = out + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * 2;
     predict(dg[1], dg[0], dg[2], dg[3], 0, (double)N[0], p);
@@ -640,14 +703,14 @@ static void fit_taxon(const uint32_t* y, const uint32_t* N, const uint32_t* mm,
   }
   /* reverse (fits.py:333-350); D_max_reverse evaluated on data_forward (:343-348) */
   out[MDFIT_F_N_SIGMA_REVERSE] =
-      n_sigma(f[3].r.ell + NHALF, f[5].r.ell + NHALF, NHALF);
+      n_sigma(ell[3] + NHALF, ell[5] + NHALF, NHALF);
   {
     const double* dg = out + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * 3;
     predict(dg[1], dg[0], dg[2], dg[3], 0, (double)N[0], p);
     out[MDFIT_F_D_MAX_REVERSE] = p[0];
     out[MDFIT_F_Q_MEAN_REVERSE] = dg[0];
   }
-  out[MDFIT_F_ASYMMETRY] = asymmetry(f[0].r.ell, f[2].r.ell, f[3].r.ell);
+  out[MDFIT_F_ASYMMETRY] = asymmetry(ell[0], ell[2], ell[3]);
   if (mm) {
     double nz[3];
     noise(mm, nz);
