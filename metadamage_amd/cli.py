@@ -78,7 +78,16 @@ def cli_fit(
         raise typer.BadParameter("--inference must be nuts or map")
     cfg = utils.Config(**d_cfg)
     cfg.add_filenames(filenames)
-    main(filenames, cfg)
+    # launched by torchrun (WORLD_SIZE > 1): one rank per GPU, the rank's GPU
+    # selected before any device call, RCCL process group; main() then deals
+    # files or shards taxa over the ranks and rank 0 writes the shared results
+    from .distributed import init_from_env, shutdown
+
+    init_from_env()
+    try:
+        main(filenames, cfg)
+    finally:
+        shutdown()
 
 
 @cli_app.command("dashboard")

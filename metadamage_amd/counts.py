@@ -160,11 +160,13 @@ CACHE_KEYS = ["min_alignments", "min_y_sum", "substitution_bases_forward", "subs
               "shortname", "filename"]
 
 
-def load_counts(cfg, writer=None):
+def load_counts(cfg, writer=None, save=True):
     """counts.py:276-306: reuse counts/<shortname>.parquet when its metadata
     matches on CACHE_KEYS and --forced is off; else compute and save (on the
     `writer` executor when one is given: main() overlaps the write with the
-    next stages)."""
+    next stages).  save=False computes without writing (the ranks of a
+    taxon-sharded job other than rank 0 need the table, not another copy of
+    the file)."""
     parquet = io.Parquet(cfg.filename_counts)
     if parquet.exists(cfg.forced):
         if utils.metadata_is_similar(parquet.load_metadata(), cfg.to_dict(), include=CACHE_KEYS):
@@ -174,7 +176,8 @@ def load_counts(cfg, writer=None):
             return df_counts
     logger.info("Creating DataFrame, please wait.")
     df_counts = compute_counts(cfg)
-    _save(writer, parquet, df_counts, cfg.to_dict())
+    if save:
+        _save(writer, parquet, df_counts, cfg.to_dict())
     cfg.set_number_of_fits(df_counts)
     return df_counts
 

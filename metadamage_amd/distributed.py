@@ -91,7 +91,9 @@ def gather_records(buf, n_cap: int, rank: int, world: int, group=None, async_op:
     """Gather every rank's staged gather buffer (Records.stage(), n_cap records
     each) to rank 0.
     Returns a list of `world` buffers on rank 0, None elsewhere.  This is the
-    one collective of the multi-GPU path (ncclGather semantics).
+    one collective of the multi-GPU path (ncclGather semantics).  Under the
+    gloo backend (CPU tests, or ranks sharing one GPU in a test) a device
+    buffer is staged to host first: gloo gathers host tensors only.
 
     async_op=True returns (parts, work) instead: the collective is queued
     behind the work already on the current stream and runs on the backend's
@@ -102,21 +104,70 @@ def gather_records(buf, n_cap: int, rank: int, world: int, group=None, async_op:
 
     if world == 1:
         return ([buf], None) if async_op else [buf]
+    if buf.is_cuda and dist.get_backend(group) == "gloo":
+        buf = buf.cpu()
     parts = [buf.new_empty(buf.shape) for _ in range(world)] if rank == 0 else None
     work = dist.gather(buf, gather_list=parts, dst=0, group=group, async_op=async_op)
     return (parts, work) if async_op else parts
 
 
+def all_ranks_agree(flag: bool) -> bool:
+    """True iff `flag` is true on every rank (a one-int all-reduce; world 1: flag).
+    Used so that all ranks take the same branch before a collective (e.g. a
+    cache hit must skip the fit on every rank or on none)."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return bool(flag)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t.item()))
+
+
+def init_from_env(backend: str | None = None) -> tuple[int, int]:
+    """Join the torch.distributed job described by the torchrun environment
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*): one process per GPU, the
+    rank's GPU selected BEFORE any other device call, backend "nccl" (RCCL
+    over xGMI) unless given.  WORLD_SIZE 1 (or unset): nothing to join.
+    Returns (rank, world)."""
+    rank, local, world = env_rank_world()
+    if world <= 1:
+        return 0, 1
+    import torch
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    backend = backend or "nccl"
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+    return dist.get_rank(), dist.get_world_size()
+
+
+def shutdown() -> None:
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def unpack_gathered(parts, n_taxa: int, world: int):
-    """Concatenate gathered shards back into df_counts order (host numpy)."""
+    """Concatenate gathered shards back into df_counts order (host numpy);
+    the parts may be device (RCCL) or host (gloo) buffers."""
     outs, preds, sts = [], [], []
     for r, part in enumerate(parts):
         lo, hi = shard_range(n_taxa, r, world)
         n_cap = part.numel() // REC_BYTES
-        p, s, o = packed_views(part, n_cap)
-        outs.append(o[: hi - lo].cpu().numpy())
-        preds.append(p[: hi - lo].cpu().numpy())
-        sts.append(s[: hi - lo].cpu().numpy())
+        p, s, o = packed_views(part.cpu(), n_cap)  # one D2H copy per part
+        outs.append(o[: hi - lo].numpy())
+        preds.append(p[: hi - lo].numpy())
+        sts.append(s[: hi - lo].numpy())
     return np.concatenate(outs), np.concatenate(preds), np.concatenate(sts)
 
 

@@ -294,6 +294,12 @@ def get_top_max_fits(df_counts, N_fits):
     return df_counts
 
 
+def _rank() -> int:
+    import torch.distributed as dist
+
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
 CACHE_KEYS = ["min_alignments", "min_y_sum", "substitution_bases_forward", "substitution_bases_reverse",
               "N_fits", "shortname", "filename", "inference"]
 
@@ -301,14 +307,22 @@ CACHE_KEYS = ["min_alignments", "min_y_sum", "substitution_bases_forward", "subs
 def get_fits(df_counts, cfg, opts=None, shard=True, writer=None):
     """fits.py:754-807.  shard: split the taxa over the torch.distributed ranks
     (rank 0 gathers and saves); writer: an executor for the parquet saves."""
+    from .distributed import all_ranks_agree
+
     parquet_fit_results = io.Parquet(cfg.filename_fit_results)
     parquet_fit_predictions = io.Parquet(cfg.filename_fit_predictions)
+    hit = False
     if parquet_fit_results.exists(cfg.forced) and parquet_fit_predictions.exists(cfg.forced):
         metadata_cfg = cfg.to_dict()
-        if utils.metadata_is_similar(parquet_fit_results.load_metadata(), metadata_cfg, include=CACHE_KEYS) and \
-                utils.metadata_is_similar(parquet_fit_predictions.load_metadata(), metadata_cfg, include=CACHE_KEYS):
-            logger.info("Fit: Loading fits from parquet-file.")
-            return parquet_fit_results.load(), parquet_fit_predictions.load()
+        hit = utils.metadata_is_similar(parquet_fit_results.load_metadata(), metadata_cfg, include=CACHE_KEYS) and \
+            utils.metadata_is_similar(parquet_fit_predictions.load_metadata(), metadata_cfg, include=CACHE_KEYS)
+    if shard:  # a taxon-sharded fit is collective: every rank reuses the cache or none does
+        hit = all_ranks_agree(hit)
+    if hit:
+        if shard and _rank() != 0:
+            return None, None
+        logger.info("Fit: Loading fits from parquet-file.")
+        return parquet_fit_results.load(), parquet_fit_predictions.load()
     logger.info("Fit: Generating fits and saving to file.")
     df_counts_top_N = get_top_max_fits(df_counts, cfg.N_fits)
     # fits.py:792-799

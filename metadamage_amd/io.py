@@ -10,6 +10,8 @@ which the installed pyarrow rejects; we write "2.6".
 from __future__ import annotations
 
 import json
+import os
+import threading
 from pathlib import Path
 
 import pyarrow as pa
@@ -66,8 +68,17 @@ class Parquet:
         utils.init_parent_folder(self.filename)
         table = self._add_metadata_to_table(pa.Table.from_pandas(df), metadata)
         cats = [f.name for f in table.schema if pa.types.is_dictionary(f.type)]
-        pq.write_table(table, self.filename, version=PARQUET_VERSION, use_dictionary=cats,
-                       write_statistics=cats or False)
+        # written next to the target and renamed into place: a reader (another
+        # rank's cache check, a writer thread of the next file) sees either no
+        # file or a complete one, never a half-written parquet
+        tmp = self.filename.with_name(f".{self.filename.name}.{os.getpid()}.{threading.get_ident()}.tmp")
+        try:
+            pq.write_table(table, tmp, version=PARQUET_VERSION, use_dictionary=cats,
+                           write_statistics=cats or False)
+            os.replace(tmp, self.filename)
+        finally:
+            if tmp.exists():
+                tmp.unlink()
 
     def exists(self, forced=False):
         return self.filename.exists() and not forced

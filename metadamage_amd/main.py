@@ -55,10 +55,10 @@ class _Writer:
         self.futures.clear()
 
 
-def _load(filename, cfg, writer):
+def _load(filename, cfg, writer, save=True):
     cfg_f = copy.copy(cfg)
     cfg_f.add_filename(filename)
-    return cfg_f, counts.load_counts(cfg_f, writer=writer)
+    return cfg_f, counts.load_counts(cfg_f, writer=writer, save=save)
 
 
 def main(filenames, cfg, opts=None):
@@ -72,16 +72,24 @@ def main(filenames, cfg, opts=None):
     world, rank = _world()
     shard_files = world > 1 and len(valid) >= world
     mine = valid[rank::world] if shard_files else valid
+    # taxon-sharded files are read by every rank (each packs its own shard);
+    # only rank 0 writes their counts parquet (atomically, io.Parquet.save)
+    save = shard_files or rank == 0
     results = {}
     with ThreadPoolExecutor(1) as reader, ThreadPoolExecutor(N_WRITERS) as pool:
         writer = _Writer(pool)
-        nxt = reader.submit(_load, mine[0], cfg, writer) if mine else None
+        nxt = reader.submit(_load, mine[0], cfg, writer, save) if mine else None
         for i in range(len(mine)):
             cfg_f, df_counts = nxt.result()
-            nxt = reader.submit(_load, mine[i + 1], cfg, writer) if i + 1 < len(mine) else None
+            nxt = reader.submit(_load, mine[i + 1], cfg, writer, save) if i + 1 < len(mine) else None
             cfg.add_filename(cfg_f.filename)  # the caller's cfg follows the files as in the reference
             cfg.N_tax_ids, cfg.N_fits = getattr(cfg_f, "N_tax_ids", None), cfg_f.N_fits
-            if not utils.is_df_counts_accepted(df_counts, cfg_f):
+            accepted = utils.is_df_counts_accepted(df_counts, cfg_f)
+            if not shard_files:  # every rank must skip (or fit) the file together
+                from .distributed import all_ranks_agree
+
+                accepted = all_ranks_agree(accepted)
+            if not accepted:
                 continue
             results[cfg_f.shortname] = fits.get_fits(df_counts, cfg_f, opts=opts, shard=not shard_files,
                                                      writer=writer)
