@@ -163,6 +163,17 @@ int mdfit_betabinom_logpmf(const double* y, const double* N, const double* alpha
 int mdfit_special(const double* x, int64_t n, double* out3, void* hip_stream);
 
 /*
+ * MAP predictive HPDI (MDFIT-HPDI v1): the 68 % highest-
+ * probability window [lo, hi] (integer counts, returned as double) of
+ * BetaBinomial(alpha, beta, N), the population form of numpyro's
+ * hpdi(obs/N, 0.68) over predictive draws (fits.py:112-120, 260-261).  The
+ * fit's D_max_{lower,upper}_hpdi and the pred bounds are lo/N, hi/N at the
+ * PMD-all mode.  Device pointers; N[i] = 0 -> NaN.  For parity tests.
+ */
+int mdfit_hpdi68(const double* N, const double* alpha, const double* beta, int64_t n, double* lo,
+                 double* hi, void* hip_stream);
+
+/*
  * Objective of one sub-fit at given unconstrained parameters, evaluated by
  * the fit kernel's own lane layout and code (parity tests).  Per item i:
  * model[i] (0 PMD, 1 null), subset[i] (0 all, 1 forward, 2 reverse),

@@ -67,6 +67,7 @@ EXPORTED_SYMBOLS = [
     "mdfit_workspace_bytes",
     "mdfit_betabinom_logpmf",
     "mdfit_special",
+    "mdfit_hpdi68",
     "mdfit_peak_probe",
     "mdfit_objective",
     "mdfit_nuts_potential",
@@ -131,6 +132,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.mdfit_betabinom_logpmf.restype = ctypes.c_int
     lib.mdfit_special.argtypes = [vp, i64, vp, vp]
     lib.mdfit_special.restype = ctypes.c_int
+    lib.mdfit_hpdi68.argtypes = [vp, vp, vp, i64, vp, vp, vp]
+    lib.mdfit_hpdi68.restype = ctypes.c_int
     lib.mdfit_peak_probe.argtypes = [i64, i32, vp, vp]
     lib.mdfit_peak_probe.restype = ctypes.c_int
     lib.mdfit_objective.argtypes = [vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp]

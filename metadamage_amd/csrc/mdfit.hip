@@ -12,7 +12,10 @@
 //                      warm-started at the all-position modes
 //   K3 assemble_kernel one wave per taxon: pointwise log-likelihoods at
 //                              the 6 modes, n_sigma x3, asymmetry, predictive
-//                              summaries, sums, noise (fits.py:230-376)
+//                              medians, sums, noise (fits.py:230-376)
+//   K4 hpdi_kernel     one lane per (taxon, position): the 68 % predictive
+//                      HPDI of the PMD-all mode (MDFIT-HPDI v1, mdfit_hpdi.h;
+//                      fits.py:112-120, 260-261)
 //
 // K1 work decomposition (details at fit_kernel): lane = position; a "slot"
 // (32 lanes at 1 point per lane, 16 at 2) runs either one all-position
@@ -34,6 +37,7 @@
 #include <cstring>
 
 #include "../../include/mdfit.h"
+#include "mdfit_hpdi.h"
 #include "mdfit_host.h"
 #include "mdfit_model.h"
 #include "mdfit_special.h"
@@ -462,19 +466,11 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
 // ---------------------------------------------------------------------------
 // K3: record assembly, one wave per taxon
 // ---------------------------------------------------------------------------
-// MAP predictive summary of one point (oracle: predict()).
-__device__ __forceinline__ void predict(double A, double q, double c, double phi, int k, double N,
-                                        double o[3]) {
-  if (N == 0.0) {
-    o[0] = o[1] = o[2] = NAN;
-    return;
-  }
-  double D = fma(A, powk(1.0 - q, k), c);
-  D = fmin(D, 1.0);
-  const double sd = sqrt(D * (1.0 - D) * (phi + N) / (N * (phi + 1.0)));
-  o[0] = D;
-  o[1] = clampd(D - kZ68 * sd, 0.0, 1.0);
-  o[2] = clampd(D + kZ68 * sd, 0.0, 1.0);
+// MAP predictive median of one point (oracle: predict()): D(z), NaN when N = 0
+// (the reference divides 0 draws by N = 0); the HPDI bounds are K4's.
+__device__ __forceinline__ double predict_median(double A, double q, double c, int k, double N) {
+  if (N == 0.0) return NAN;
+  return fmin(fma(A, powk(1.0 - q, k), c), 1.0);
 }
 
 // n_sigma (fits.py:194-201) over the valid lanes of G-lane groups, from each
@@ -580,17 +576,11 @@ __global__ __launch_bounds__(kWave) void assemble_kernel(
   {
     const double ellN = __shfl_xor(ellA, 32);
     const double ns = nsigma_group<32>(vA, ellA, ellN, (double)kNPos);  // fits.py:252
-    double pr[3];
-    predict(ths[0].A, ths[0].q, ths[0].c, ths[0].phi, kA, s_N[iA], pr);
-    if (lane < kNPos && pred != nullptr) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) pred[t * (MDFIT_NPRED * kNPos) + j * kNPos + lane] = (float)pr[j];
-    }
+    const double med = predict_median(ths[0].A, ths[0].q, ths[0].c, kA, s_N[iA]);
+    if (lane < kNPos && pred != nullptr) pred[t * (MDFIT_NPRED * kNPos) + lane] = (float)med;
     if (lane == 0) {
       s_rec[MDFIT_F_N_SIGMA] = ns;
-      s_rec[MDFIT_F_D_MAX] = pr[0];  // fits.py:249-250: predictive median at z = +1
-      s_rec[MDFIT_F_D_MAX_LOWER_HPDI] = pr[1];
-      s_rec[MDFIT_F_D_MAX_UPPER_HPDI] = pr[2];
+      s_rec[MDFIT_F_D_MAX] = med;  // fits.py:249-250: predictive median at z = +1
       s_rec[MDFIT_F_Q_MEAN] = ths[0].q;
       s_rec[MDFIT_F_CONCENTRATION_MEAN] = ths[0].phi;
       s_rec[MDFIT_F_D_MAX_MARGINALIZED_MEAN] = ths[0].A + ths[0].c;
@@ -609,18 +599,17 @@ __global__ __launch_bounds__(kWave) void assemble_kernel(
     const double ellB = point_ell(s_y[iB], s_N[iB], d_of(thB, pmdB, kB), thB.phi);
     const double ellN = __shfl_xor(ellB, 32);
     const double ns = nsigma_group<16>(vB, ellB, ellN, (double)kNHalf);  // fits.py:317-320, 339-342
-    double pr[3];
     // D_max_forward / _reverse: predictive median at data_forward[0]
     // (fits.py:322-327; the reverse one is evaluated on data_forward, :343-348)
-    predict(thB.A, thB.q, thB.c, thB.phi, 0, s_N[0], pr);
+    const double med = predict_median(thB.A, thB.q, thB.c, 0, s_N[0]);
     if (lane == 0) {
       s_rec[MDFIT_F_N_SIGMA_FORWARD] = ns;
-      s_rec[MDFIT_F_D_MAX_FORWARD] = pr[0];
+      s_rec[MDFIT_F_D_MAX_FORWARD] = med;
       s_rec[MDFIT_F_Q_MEAN_FORWARD] = thB.q;
     }
     if (lane == 16) {
       s_rec[MDFIT_F_N_SIGMA_REVERSE] = ns;
-      s_rec[MDFIT_F_D_MAX_REVERSE] = pr[0];
+      s_rec[MDFIT_F_D_MAX_REVERSE] = med;
       s_rec[MDFIT_F_Q_MEAN_REVERSE] = thB.q;
     }
     // asymmetry (fits.py:352-356, 204-227): PMD-all vs concat(PMD-fwd, PMD-rev);
@@ -642,6 +631,148 @@ __global__ __launch_bounds__(kWave) void assemble_kernel(
   __syncthreads();
   for (int i = lane; i < MDFIT_NOUT; i += kWave) out[t * MDFIT_NOUT + i] = s_rec[i];
   if (lane == 0) status[t] = st;
+}
+
+// ---------------------------------------------------------------------------
+// K4: 68 % predictive HPDI (MDFIT-HPDI v1, mdfit_hpdi.h) of the PMD-all mode at
+// every position (fits.py:112-120, 260-261).  K4a: one lane per (taxon,
+// position) -- neighbouring lanes hold neighbouring positions of one taxon;
+// windows of sd <= 100 points are finished there (the greedy), wide ones go to
+// a compacted list.  K4b: persistent; each lane runs one wide window's state
+// machine at a time and refills from the list (mdfit_hpdi.h).
+// Sources: the fit record (kFit: PMD-all (q, A, c, phi) + N; pred == nullptr
+// -> only z = +1, the D_max_{lower,upper}_hpdi columns) or plain arrays
+// (mdfit_hpdi68, parity tests).
+// ---------------------------------------------------------------------------
+constexpr int kHpdiCtr = 16;  // workspace ints: [16] wide count, [17] claim counter (zeroed by K0)
+
+struct HpdiIO {
+  // kFit
+  const uint32_t* gN;
+  double* out;
+  float* pred;
+  int per;  // positions per taxon written (30, or 1 without pred)
+  // arrays
+  const double *N, *a, *b;
+  double *lo, *hi;
+};
+
+template <bool kFit>
+__device__ __forceinline__ void hpdi_write(const HpdiIO& io, int64_t item, double N, double lo, double hi) {
+  if (kFit) {
+    const int64_t t = item / io.per;
+    const int i = (int)(item - t * io.per);
+    const double fl = N > 0.0 ? lo / N : NAN, fh = N > 0.0 ? hi / N : NAN;
+    if (io.pred != nullptr) {
+      io.pred[t * (MDFIT_NPRED * kNPos) + 1 * kNPos + i] = (float)fl;
+      io.pred[t * (MDFIT_NPRED * kNPos) + 2 * kNPos + i] = (float)fh;
+    }
+    if (i == 0) {
+      io.out[t * MDFIT_NOUT + MDFIT_F_D_MAX_LOWER_HPDI] = fl;
+      io.out[t * MDFIT_NOUT + MDFIT_F_D_MAX_UPPER_HPDI] = fh;
+    }
+  } else {
+    io.lo[item] = lo;
+    io.hi[item] = hi;
+  }
+}
+
+template <bool kFit>
+__global__ __launch_bounds__(kWave) void hpdi_prep_kernel(HpdiIO io, int64_t n_items, int* __restrict__ ctr,
+                                                          hpdi::WideRec* __restrict__ recs) {
+  const int64_t item = (int64_t)blockIdx.x * kWave + threadIdx.x;
+  const bool valid = item < n_items;
+  double N = 0.0, a = 0.0, b = 0.0;
+  bool skip = true;
+  if (valid) {
+    if (kFit) {
+      const int64_t t = item / io.per;
+      const int i = (int)(item - t * io.per);
+      const double* dg = io.out + t * MDFIT_NOUT + MDFIT_F_DIAG;  // PMD-all: (q, A, c, phi)
+      const double q = dg[0], A = dg[1], c = dg[2], phi = dg[3];
+      N = (double)io.gN[t * kLD + i];
+      if (N > 0.0 && !isnan(q)) {
+        const int k = i < kNHalf ? i : i - kNHalf;
+        const double D = fmin(fma(A, powk(1.0 - q, k), c), 1.0);
+        a = D * phi;
+        b = (1.0 - D) * phi;
+        skip = false;
+      }
+    } else {
+      N = io.N[item];
+      a = io.a[item];
+      b = io.b[item];
+      skip = !(N > 0.0);
+    }
+  }
+  bool wide = false;
+  hpdi::WideRec rec;
+  if (valid) {
+    double lo = NAN, hi = NAN;
+    if (!skip) wide = !hpdi::prep_position(N, a, b, lo, hi, rec);
+    if (!wide) hpdi_write<kFit>(io, item, N, lo, hi);
+  }
+  const unsigned long long m = __ballot(wide);
+  if (m == 0ull) return;
+  int base = 0;
+  if (threadIdx.x == 0) base = atomicAdd(ctr, __popcll(m));
+  base = __shfl(base, 0);
+  if (wide) {
+    rec.item = item;
+    recs[base + __popcll(m & ((1ull << threadIdx.x) - 1ull))] = rec;
+  }
+}
+
+#ifndef MDFIT_HPDI_WPE
+#define MDFIT_HPDI_WPE 1  // minimum waves per SIMD the register budget allows (development A/B)
+#endif
+template <bool kFit>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPDI_WPE))) void hpdi_wide_kernel(HpdiIO io, int* __restrict__ ctr,
+                                                          const hpdi::WideRec* __restrict__ recs) {
+  const int lane = threadIdx.x;
+  const int n_wide = __builtin_nontemporal_load(ctr);  // written by K4a (stream-ordered)
+  hpdi::Wide W;
+  int64_t item = -1;
+  bool busy = false, drained = false, have = false;
+  W.phase = hpdi::W_DONE;
+  for (;;) {
+    // free lanes claim the next wide windows (one atomic per wave-trip)
+    const bool need = !busy && !drained;
+    if (__any(need)) {
+      const unsigned long long m = __ballot(need);
+      int base = 0;
+      if (lane == 0) base = atomicAdd(ctr + 1, __popcll(m));
+      base = __shfl(base, 0);
+      if (need) {
+        const int my = base + __popcll(m & ((1ull << lane) - 1ull));
+        if (my < n_wide) {
+          const hpdi::WideRec r = recs[my];
+          hpdi::wide_load(W, r);
+          item = r.item;
+          busy = true;
+          have = false;
+        } else {
+          drained = true;
+        }
+      }
+    }
+    if (!__any(busy)) break;
+    bool req = false;
+    if (busy) {
+      req = hpdi::wide_step(W, have);
+      if (!req) {
+        hpdi_write<kFit>(io, item, W.P.N, W.A, W.B);
+        busy = false;
+      }
+    }
+    // the one evaluation site: ln p(x) - ln p(m) and its derivative
+    if (req) {
+      double sx;
+      W.res_g = hpdi::gfun<true>(W.P, W.req_x, sx);
+      W.res_s = sx;
+    }
+    have = req;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -810,6 +941,25 @@ void prof_record(int slot, hipStream_t s) {
 }
 }  // namespace
 
+namespace {
+// HPDI wide-window records follow the 256 B of counters in the MAP workspace
+mdfit::hpdi::WideRec* hpdi_recs(void* ws) {
+  return reinterpret_cast<mdfit::hpdi::WideRec*>(static_cast<char*>(ws) + 256);
+}
+
+template <bool kFit>
+int launch_hpdi(const mdfit::HpdiIO& io, int64_t n_items, int* ctr, mdfit::hpdi::WideRec* recs, hipStream_t s) {
+  if (n_items == 0) return 0;
+  hipLaunchKernelGGL(mdfit::hpdi_prep_kernel<kFit>, dim3((unsigned)((n_items + mdfit::kWave - 1) / mdfit::kWave)),
+                     dim3(mdfit::kWave), 0, s, io, n_items, ctr, recs);
+  if (int rc = check_launch("hpdi_prep_kernel")) return rc;
+  // persistent: no more waves than are resident, and no more than the items need
+  const int64_t g = fit_grid(mdfit::hpdi_wide_kernel<kFit>, n_items, mdfit::kWave);
+  hipLaunchKernelGGL(mdfit::hpdi_wide_kernel<kFit>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, io, ctr, recs);
+  return check_launch("hpdi_wide_kernel");
+}
+}  // namespace
+
 void mdfit::host::prof_mark(int slot, hipStream_t s) { prof_record(slot, s); }
 
 extern "C" {
@@ -865,7 +1015,9 @@ int64_t mdfit_workspace_bytes(int64_t n_taxa, const mdfit_opts* opts) {
   mdfit_default_opts(&o);
   if (opts) o = *opts;
   if (o.mode == MDFIT_MODE_NUTS) return mdfit::nuts::workspace_bytes(n_taxa, o.num_samples);
-  return 256;  // the 8 per-XCD queue counters (int32), padded
+  // the 8 per-XCD queue counters + the HPDI list counters (int32, 256 B), then
+  // room for every position's wide-window record (MDFIT-HPDI v1)
+  return 256 + n_taxa * mdfit::kNPos * (int64_t)sizeof(mdfit::hpdi::WideRec);
 }
 
 int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t n_taxa,
@@ -915,6 +1067,14 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   hipLaunchKernelGGL(mdfit::assemble_kernel, dim3((unsigned)n_taxa), dim3(mdfit::kWave), 0, s, y, N,
                      mm, n_taxa, out, pred, status);
   if (int rc = check_launch("assemble_kernel")) return rc;
+  {
+    mdfit::HpdiIO io{};
+    io.gN = N;
+    io.out = out;
+    io.pred = pred;
+    io.per = pred != nullptr ? mdfit::kNPos : 1;
+    if (int rc = launch_hpdi<true>(io, n_taxa * io.per, ws + mdfit::kHpdiCtr, hpdi_recs(workspace), s)) return rc;
+  }
   prof_record(3, s);
   if (g_prof.on && g_prof.n < kProfMax) ++g_prof.n;
   return 0;
@@ -930,6 +1090,26 @@ int mdfit_betabinom_logpmf(const double* y, const double* N, const double* alpha
   hipLaunchKernelGGL(mdfit::betabinom_kernel, dim3(blocks), dim3(256), 0,
                      (hipStream_t)hip_stream, y, N, alpha, beta, n, out, grad);
   return check_launch("betabinom_kernel");
+}
+
+int mdfit_hpdi68(const double* N, const double* alpha, const double* beta, int64_t n, double* lo,
+                 double* hi, void* hip_stream) {
+  if (n < 0 || (n > 0 && (!N || !alpha || !beta || !lo || !hi))) return set_err(MDFIT_E_ARG, "bad arguments");
+  if (n == 0) return 0;
+  hipStream_t s = (hipStream_t)hip_stream;
+  void* ws = nullptr;
+  const size_t bytes = 256 + (size_t)n * sizeof(mdfit::hpdi::WideRec);
+  if (hipMallocAsync(&ws, bytes, s) != hipSuccess) return set_err(MDFIT_E_HIP, "hipMallocAsync");
+  if (hipMemsetAsync(ws, 0, 256, s) != hipSuccess) return set_err(MDFIT_E_HIP, "hipMemsetAsync");
+  mdfit::HpdiIO io{};
+  io.N = N;
+  io.a = alpha;
+  io.b = beta;
+  io.lo = lo;
+  io.hi = hi;
+  int rc = launch_hpdi<false>(io, n, static_cast<int*>(ws) + mdfit::kHpdiCtr, hpdi_recs(ws), s);
+  (void)hipFreeAsync(ws, s);
+  return rc;
 }
 
 int mdfit_special(const double* x, int64_t n, double* out3, void* hip_stream) {

@@ -21,7 +21,6 @@ constexpr int kNPos = MDFIT_NPOS;
 constexpr int kNHalf = MDFIT_NHALF;
 constexpr int kLD = MDFIT_LD;
 constexpr int kNMM = MDFIT_NMM;
-constexpr double kZ68 = 0.994457883209753;  // Phi^-1(0.84)
 
 // u = (logit q, logit A, c, log delta): c on its own scale (see oracle).
 constexpr double kULo[4] = {-25.0, -25.0, 0.0, -25.0};

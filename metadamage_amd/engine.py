@@ -157,6 +157,23 @@ def betabinom_logpmf(y, N, a, b, device="cuda"):
     return o.cpu().numpy(), g.cpu().numpy()
 
 
+def hpdi68(N, a, b, device="cuda"):
+    """68 % predictive window [lo, hi] of BetaBinomial(a, b, N) on the device
+    (MDFIT-HPDI v1, mdfit_hpdi68; parity tests)."""
+    torch = _torch()
+    lib = _lib.load()
+    shape = np.broadcast(N, a, b).shape
+    ts = [torch.as_tensor(np.ascontiguousarray(np.broadcast_to(v, shape), dtype=np.float64).ravel(), device=device)
+          for v in (N, a, b)]
+    n = ts[0].numel()
+    lo = torch.empty(n, dtype=torch.float64, device=device)
+    hi = torch.empty(n, dtype=torch.float64, device=device)
+    _lib.check(lib.mdfit_hpdi68(*[ctypes.c_void_p(t.data_ptr()) for t in ts], n, ctypes.c_void_p(lo.data_ptr()),
+                                ctypes.c_void_p(hi.data_ptr()), _stream_handle(torch)))
+    torch.cuda.current_stream().synchronize()
+    return lo.cpu().numpy(), hi.cpu().numpy()
+
+
 def peak_probe(n_waves: int, iters: int, stream=None):
     """Launch the register-only point-evaluation probe; returns the sink tensor."""
     torch = _torch()

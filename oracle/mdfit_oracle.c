@@ -602,23 +602,29 @@ static void noise(const uint32_t* mm, double out3[3]) {
   }
 }
 
-#define Z68 0.994457883209753 /* Phi^-1(0.84): 68 % central interval */
+#include "mdfit_hpdi.c"
 
-/* MAP predictive summary at point i: median := D(z), HPDI := D -/+ Z68 * sd of
- * BetaBinomial(D phi, (1-D) phi, N)/N, clipped to [0,1]; NaN when N = 0
- * (the reference divides 0 draws by N = 0, fits.py:115). */
+/* MAP predictive summary at point i (fits.py:112-120 with the mode as the one
+ * posterior sample): median := D(z); HPDI := the 68 % window [lo, hi] / N of
+ * BetaBinomial(D phi, (1-D) phi, N) (MDFIT-HPDI v1, mdfit_hpdi.c); NaN when
+ * N = 0 (the reference divides 0 draws by N = 0, fits.py:115).  want_hpdi = 0:
+ * the median only (D_max_forward / _reverse). */
 static void predict(double A, double q, double c, double phi, int k, double N,
-                    double o[3]) {
+                    double o[3], int want_hpdi) {
   if (N == 0) {
     o[0] = o[1] = o[2] = NAN;
     return;
   }
   double D = A * pow(1.0 - q, k) + c;
   if (D > 1.0) D = 1.0;
-  double sd = sqrt(D * (1.0 - D) * (phi + N) / (N * (phi + 1.0)));
   o[0] = D;
-  o[1] = clampd(D - Z68 * sd, 0.0, 1.0);
-  o[2] = clampd(D + Z68 * sd, 0.0, 1.0);
+  o[1] = o[2] = NAN;
+  if (want_hpdi) {
+    double lo, hi;
+    hp_window(N, D * phi, (1.0 - D) * phi, &lo, &hi);
+    o[1] = lo / N;
+    o[2] = hi / N;
+  }
 }
 
 static void fit_taxon(const uint32_t* y, const uint32_t* N, const uint32_t* mm,
@@ -662,7 +668,7 @@ static void fit_taxon(const uint32_t* y, const uint32_t* N, const uint32_t* mm,
   double qa = out[MDFIT_F_DIAG + 0], Aa = out[MDFIT_F_DIAG + 1];
   double ca = out[MDFIT_F_DIAG + 2], pa = out[MDFIT_F_DIAG + 3];
   for (int i = 0; i < NPOS; i++) {
-    predict(Aa, qa, ca, pa, kpos(i), (double)N[i], p);
+    predict(Aa, qa, ca, pa, kpos(i), (double)N[i], p, 1);
     if (pred)
       for (int r = 0; r < 3; r++) pred[r * NPOS + i] = (float)p[r];
     if (i == 0) {
@@ -697,7 +703,7 @@ static void fit_taxon(const uint32_t* y, const uint32_t* N, const uint32_t* mm,
   out[MDFIT_F_N_SIGMA_FORWARD] = n_sigma(ell[2], ell[4], NHALF);
   {
     const double* dg = out + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * 2;
-    predict(dg[1], dg[0], dg[2], dg[3], 0, (double)N[0], p);
+    predict(dg[1], dg[0], dg[2], dg[3], 0, (double)N[0], p, 0);
     out[MDFIT_F_D_MAX_FORWARD] = p[0];
     out[MDFIT_F_Q_MEAN_FORWARD] = dg[0];
   }
@@ -706,7 +712,7 @@ static void fit_taxon(const uint32_t* y, const uint32_t* N, const uint32_t* mm,
       n_sigma(ell[3] + NHALF, ell[5] + NHALF, NHALF);
   {
     const double* dg = out + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * 3;
-    predict(dg[1], dg[0], dg[2], dg[3], 0, (double)N[0], p);
+    predict(dg[1], dg[0], dg[2], dg[3], 0, (double)N[0], p, 0);
     out[MDFIT_F_D_MAX_REVERSE] = p[0];
     out[MDFIT_F_Q_MEAN_REVERSE] = dg[0];
   }

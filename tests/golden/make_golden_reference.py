@@ -28,7 +28,9 @@ scratch cwd (metadamage/__init__.py creates ./logs):
       (fit_mcmc, compute_log_likelihood, get_y_average_and_hpdi,
       get_mean_of_variable are replaced by the MAP mode found by the scipy
       optimiser of make_golden_scipy.py), so the reference's own code decides
-      column order, the 15/15 split and the D_max_reverse-on-data_forward quirk;
+      column order, the 15/15 split and the D_max_reverse-on-data_forward quirk
+      (the predictive HPDI comes from scipy's BetaBinomial pmf:
+      make_golden_hpdi.hpdi_window, independent of the oracle and the kernel);
   (6) make_df_fit_results_from_fit_results / make_df_fit_predictions_from_d_fits
       column lists (fits.py:632-680).
 
@@ -268,20 +270,25 @@ def main():
                 + special.gammaln(y + a) + special.gammaln(N - y + b) - special.gammaln(N + phi)
                 - special.gammaln(a) - special.gammaln(b) + special.gammaln(phi))
 
-    Z68 = 0.994457883209753
+    import make_golden_hpdi as mgh  # scipy's shortest 68 % window of the predictive BetaBinomial
 
     def map_predictive(mcmc, data, func=np.median, return_hpdi=True):
+        """get_y_average_and_hpdi (fits.py:112-120) with the mode as the one
+        posterior sample: median := D(z); HPDI := the shortest window of
+        BetaBinomial(D phi, (1-D) phi, N) / N holding 68 % (scipy pmf)."""
         q, A, c, phi = mcmc.theta
         N = data["N"].astype(float)
         k = np.abs(data["z"]) - 1.0
         D = np.minimum(A * (1 - q) ** k + c, 1.0)
-        with np.errstate(divide="ignore", invalid="ignore"):
-            sd = np.sqrt(D * (1 - D) * (phi + N) / (N * (phi + 1)))
-            med = np.where(N > 0, D, np.nan)
-            lo = np.where(N > 0, np.clip(D - Z68 * sd, 0, 1), np.nan)
-            hi = np.where(N > 0, np.clip(D + Z68 * sd, 0, 1), np.nan)
+        med = np.where(N > 0, D, np.nan)
         if not return_hpdi:
             return med
+        lo = np.full_like(N, np.nan)
+        hi = np.full_like(N, np.nan)
+        for i in range(N.size):
+            if N[i] > 0:
+                wl, wh = mgh.hpdi_window(N[i], D[i] * phi, (1 - D[i]) * phi)
+                lo[i], hi[i] = wl / N[i], wh / N[i]
         return med, np.stack([lo, hi])
 
     fits.fit_mcmc = lambda mcmc, data, seed=0: mcmc.run(data)

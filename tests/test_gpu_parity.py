@@ -111,6 +111,39 @@ def oracle_lib_init(oracle_lib, model, subset, y30, N30):
 
 
 # --------------------------------------------------------------------------
+# MAP predictive HPDI (MDFIT-HPDI v1): the kernel's window vs scipy and the oracle
+# --------------------------------------------------------------------------
+def test_hpdi_kernel_vs_scipy_and_oracle(engine, oracle_lib):
+    from pathlib import Path
+
+    g = np.load(Path(__file__).resolve().parent / "golden" / "hpdi_golden.npz")
+    lo, hi = engine.hpdi68(g["N"], g["a"], g["b"])
+    small = g["N"] <= 1e5
+    bad = np.where(small & ((lo != g["lo"]) | (hi != g["hi"])))[0]
+    assert bad.size == 0, [(g["N"][i], g["a"][i], g["b"][i], lo[i], hi[i], g["lo"][i], g["hi"][i]) for i in bad[:5]]
+    rel = np.maximum(np.abs(lo - g["lo"]) / np.maximum(g["lo"], 1), np.abs(hi - g["hi"]) / np.maximum(g["hi"], 1))
+    assert rel.max() < 1e-5, rel.max()
+    # 20k random windows (N up to 1e9 per position, phi down to 2+) vs the
+    # oracle's spec.  (Beyond 1e9 with phi < 3 -- a nearly flat pmf whose window
+    # spans ~1e9 counts -- a 1e-7 relative rounding of ln p moves the ends by
+    # ~1e4 counts: kernel and oracle then agree to ~1.3e-4; the
+    # N = 4e9 fit edge case below stays in the suite.)
+    rng = np.random.default_rng(17)
+    n = 20000
+    N = np.floor(np.exp(rng.uniform(0.0, np.log(1e9), n)))
+    D = np.exp(rng.uniform(np.log(1e-4), np.log(0.99), n))
+    phi = np.exp(rng.uniform(np.log(2.0001), np.log(1e5), n))
+    lo, hi = engine.hpdi68(N, D * phi, (1 - D) * phi)
+    olo, ohi = oracle_lib.hpdi68(N, D * phi, (1 - D) * phi)
+    # the reported bounds lo/N, hi/N under the result columns' bar (mixed_rel:
+    # 1e-4 relative, 1e-6 absolute below 1e-2): a one-count difference at the
+    # small end of a window ~1e8 counts wide is a rounding of its ~1e-10 mass
+    rel = np.maximum(mixed_rel(lo / N, olo / N), mixed_rel(hi / N, ohi / N))
+    assert rel.max() < RTOL, (rel.max(), N[rel.argmax()], D[rel.argmax()], phi[rel.argmax()])
+    assert ((lo == olo) & (hi == ohi)).mean() > 0.999
+
+
+# --------------------------------------------------------------------------
 # the fit vs the oracle
 # --------------------------------------------------------------------------
 def test_fixture_taxa_vs_oracle(engine, oracle_lib, ref_golden):

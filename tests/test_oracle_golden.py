@@ -10,6 +10,8 @@
 
 from __future__ import annotations
 
+from pathlib import Path
+
 import numpy as np
 import pytest
 
@@ -172,3 +174,56 @@ def test_packing_vs_group_to_numpyro_data(ref_golden):
     for name in ("data_ancient", "data_control", "synthetic", "synthetic_strict", "synthetic_CA_GT"):
         z = ref_golden[f"{name}__z"]
         assert (z == np.r_[np.arange(1, 16), -np.arange(1, 16)]).all()
+
+
+# --------------------------------------------------------------------------
+# MAP predictive HPDI (MDFIT-HPDI v1, oracle/mdfit_hpdi.c)
+# --------------------------------------------------------------------------
+def _window_rel(lo, hi, rlo, rhi):
+    """relative error of the reported bounds lo/N, hi/N (counts >= 1 as scale)"""
+    return np.maximum(np.abs(lo - rlo) / np.maximum(rlo, 1.0), np.abs(hi - rhi) / np.maximum(rhi, 1.0))
+
+
+def test_hpdi_vs_scipy_golden(oracle_lib):
+    """Both the spec (greedy / Newton + Euler-Maclaurin + fix-up) and the
+    point-by-point definition against scipy's sort-based shortest 68 % window
+    (tests/golden/make_golden_hpdi.py): identical integers up to N = 1e5, and
+    within 1e-5 relative beyond (the wide, near-flat windows where a rounding
+    of the pmf decides between neighbouring counts)."""
+    g = np.load(Path(__file__).resolve().parent / "golden" / "hpdi_golden.npz")
+    for greedy in (False, True):
+        lo, hi = oracle_lib.hpdi68(g["N"], g["a"], g["b"], greedy=greedy)
+        small = g["N"] <= 1e5
+        assert np.array_equal(lo[small], g["lo"][small]) and np.array_equal(hi[small], g["hi"][small]), greedy
+        rel = _window_rel(lo, hi, g["lo"], g["hi"])
+        assert rel.max() < 1e-5, (greedy, rel.max())
+        assert ((lo == g["lo"]) & (hi == g["hi"])).mean() > 0.98
+
+
+def test_hpdi_spec_matches_the_definition():
+    """The spec against the greedy definition on 20k random (N, D, phi) over
+    the whole input range (N up to 3e6, phi down to 2+): within 1e-4 of the
+    bounds everywhere (the bar of the fit outputs), identical integers for
+    >= 99.9 %."""
+    from oracle.oracle import OracleLib
+
+    o = OracleLib()
+    rng = np.random.default_rng(7)
+    n = 20000
+    N = np.floor(np.exp(rng.uniform(np.log(1), np.log(3e6), n)))
+    D = np.exp(rng.uniform(np.log(1e-4), np.log(0.99), n))
+    phi = np.exp(rng.uniform(np.log(2.0001), np.log(1e5), n))
+    lo, hi = o.hpdi68(N, D * phi, (1 - D) * phi)
+    glo, ghi = o.hpdi68(N, D * phi, (1 - D) * phi, greedy=True)
+    assert _window_rel(lo, hi, glo, ghi).max() < 1e-4
+    assert ((lo == glo) & (hi == ghi)).mean() > 0.999
+
+
+def test_hpdi_edges(oracle_lib):
+    """N = 0 -> NaN; alpha -> 0 (D = 0): the point mass at 0; one count;
+    the mode alone holding 68 %."""
+    lo, hi = oracle_lib.hpdi68([0.0, 5.0, 1.0, 1e6], [1.0, 0.0, 0.5, 1e-9], [1.0, 3.0, 0.5 + 2.0, 50.0])
+    assert np.isnan(lo[0]) and np.isnan(hi[0])
+    assert (lo[1], hi[1]) == (0.0, 0.0)
+    assert lo[2] == 0.0 and hi[2] in (0.0, 1.0)
+    assert (lo[3], hi[3]) == (0.0, 0.0)
