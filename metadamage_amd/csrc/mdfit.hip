@@ -723,55 +723,17 @@ __global__ __launch_bounds__(kWave) void hpdi_prep_kernel(HpdiIO io, int64_t n_i
   }
 }
 
-#ifndef MDFIT_HPDI_WPE
-#define MDFIT_HPDI_WPE 1  // minimum waves per SIMD the register budget allows (development A/B)
-#endif
+// one lane per wide window; the records are in K4a's append order, so a wave's
+// lanes mostly hold neighbouring positions of the same taxa (similar work)
 template <bool kFit>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPDI_WPE))) void hpdi_wide_kernel(HpdiIO io, int* __restrict__ ctr,
+__global__ __launch_bounds__(kWave) void hpdi_wide_kernel(HpdiIO io, const int* __restrict__ ctr,
                                                           const hpdi::WideRec* __restrict__ recs) {
-  const int lane = threadIdx.x;
-  const int n_wide = __builtin_nontemporal_load(ctr);  // written by K4a (stream-ordered)
-  hpdi::Wide W;
-  int64_t item = -1;
-  bool busy = false, drained = false, have = false;
-  W.phase = hpdi::W_DONE;
-  for (;;) {
-    // free lanes claim the next wide windows (one atomic per wave-trip)
-    const bool need = !busy && !drained;
-    if (__any(need)) {
-      const unsigned long long m = __ballot(need);
-      int base = 0;
-      if (lane == 0) base = atomicAdd(ctr + 1, __popcll(m));
-      base = __shfl(base, 0);
-      if (need) {
-        const int my = base + __popcll(m & ((1ull << lane) - 1ull));
-        if (my < n_wide) {
-          const hpdi::WideRec r = recs[my];
-          hpdi::wide_load(W, r);
-          item = r.item;
-          busy = true;
-          have = false;
-        } else {
-          drained = true;
-        }
-      }
-    }
-    if (!__any(busy)) break;
-    bool req = false;
-    if (busy) {
-      req = hpdi::wide_step(W, have);
-      if (!req) {
-        hpdi_write<kFit>(io, item, W.P.N, W.A, W.B);
-        busy = false;
-      }
-    }
-    // the one evaluation site: ln p(x) - ln p(m) and its derivative
-    if (req) {
-      double sx;
-      W.res_g = hpdi::gfun<true>(W.P, W.req_x, sx);
-      W.res_s = sx;
-    }
-    have = req;
+  const int n_wide = ctr[0];  // written by K4a (stream-ordered)
+  for (int64_t i = (int64_t)blockIdx.x * kWave + threadIdx.x; i < n_wide; i += (int64_t)gridDim.x * kWave) {
+    const hpdi::WideRec r = recs[i];
+    double lo, hi;
+    hpdi::wide_window(r, lo, hi);
+    hpdi_write<kFit>(io, r.item, r.N, lo, hi);
   }
 }
 
@@ -953,7 +915,8 @@ int launch_hpdi(const mdfit::HpdiIO& io, int64_t n_items, int* ctr, mdfit::hpdi:
   hipLaunchKernelGGL(mdfit::hpdi_prep_kernel<kFit>, dim3((unsigned)((n_items + mdfit::kWave - 1) / mdfit::kWave)),
                      dim3(mdfit::kWave), 0, s, io, n_items, ctr, recs);
   if (int rc = check_launch("hpdi_prep_kernel")) return rc;
-  // persistent: no more waves than are resident, and no more than the items need
+  // no more waves than are resident, and no more than the items need (the
+  // kernel strides over the wide list, whose length only the device knows)
   const int64_t g = fit_grid(mdfit::hpdi_wide_kernel<kFit>, n_items, mdfit::kWave);
   hipLaunchKernelGGL(mdfit::hpdi_wide_kernel<kFit>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, io, ctr, recs);
   return check_launch("hpdi_wide_kernel");

@@ -36,6 +36,10 @@
 namespace mdfit {
 namespace hpdi {
 
+#ifndef MDFIT_HPDI_UNROLL
+#define MDFIT_HPDI_UNROLL 1
+#endif
+
 constexpr double kMass = 0.68;
 constexpr double kSigGreedy = 100.0;
 constexpr double kT0 = -0.49447329849;  // -Z68^2 / 2
@@ -217,45 +221,14 @@ __device__ __forceinline__ bool prep_position(double N, double a, double b, doub
 }
 
 // ---------------------------------------------------------------------------
-// K4b: the wide-window state machine (oracle: hp_window's Newton branch)
+// K4b: a wide window (oracle: hp_window's Newton branch), straight-line per
+// lane.  Every lane of a wave runs the same loops (the windows differ only in
+// trip counts), and each pmf evaluation sits at one site per loop.
 // ---------------------------------------------------------------------------
-// phases of the main machine
-enum : int {
-  W_G0 = 0, W_GN, W_DECIDE,
-  W_ONE_TOP, W_ONE_FX,                         // one-sided Newton
-  W_TWO_TOP, W_TWO_ROOTR, W_TWO_MASS, W_TWO_SL, W_TWO_SR,  // two-sided Newton
-  W_FIX_A, W_FIX_B, W_FIX_WALK, W_DONE,
-  // sub-machines (return to `ret`)
-  W_ROOT, W_MASS_BEGIN, W_MASS_HR, W_MASS_MID, W_MASS_NODES, W_MASS_ENDA, W_MASS_ENDB,
-  W_EXACT_WALK
-};
-
-struct Wide {
-  Pmf P;
-  double sd, mu, g0, gN, t, tL, tH, x, lb, hb, xl, xr, Dp, mv, M, A, B;
-  int phase, ret, it, one, cl, cr;
-  // root sub-machine
-  double r_lo, r_hi, r_x;
-  int r_it, r_rising, r_ret;
-  // mass sub-machine
-  double m_A1, m_B1, m_tot, m_I, m_c, m_e, fA, sA;
-  double p_u0, p_u1, p_v0, p_v1, p_h, p_cm;
-  int p_part, p_sub, p_j, p_k, p_i, p_nl, p_nr, m_ret, m_mode;
-  // exact-walk sub-machine (sum_{y=ew_y..ew_end} p(y)/p(m))
-  double ew_y, ew_end, ew_v, ew_s;
-  int ew_ret;
-  // fix-up
-  double pA, pB, pl, pr;
-  // the pending evaluation
-  double req_x;
-  int req_s;
-  double res_g, res_s;
-};
-
-__device__ __forceinline__ void wide_load(Wide& W, const WideRec& r) {
-  set_pmf(W.P, r.N, r.a, r.b, r.m, r.pm);
+__device__ __forceinline__ void load_pmf(Pmf& P, const WideRec& r) {
+  set_pmf(P, r.N, r.a, r.b, r.m, r.pm);
   const double z[4] = {r.m + r.a, r.m + 1.0, r.N - r.m + r.b, r.N - r.m + 1.0};
-  Anchor* an[4] = {&W.P.Aa, &W.P.A1, &W.P.Bb, &W.P.B1};
+  Anchor* an[4] = {&P.Aa, &P.A1, &P.Bb, &P.B1};
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     an[j]->z = z[j];
@@ -263,492 +236,277 @@ __device__ __forceinline__ void wide_load(Wide& W, const WideRec& r) {
     an[j]->iz = r.iz[j];
     an[j]->c = r.c[j];
   }
-  W.sd = r.sd;
-  W.mu = r.mu;
-  W.phase = W_G0;
 }
 
-// the sub-part (p_part, p_sub) of the mass integral: bounds and variable
-__device__ __forceinline__ bool part_setup(Wide& W) {
-  // parts: 0 = [A1, c], 1 = [c, B1]; a part with both ends near a support end
-  // splits at its midpoint into sub-parts 0 / 1 (oracle: hp_part)
-  for (; W.p_part < 2; ++W.p_part, W.p_sub = 0) {
-    const double u0 = W.p_part == 0 ? W.m_A1 : W.m_c;
-    const double u1 = W.p_part == 0 ? W.m_c : W.m_B1;
+// sum_{y=A}^{B} p(y)/p(m) by the recurrence from one evaluation at A
+__device__ __forceinline__ double walk_sum(const Pmf& P, double A, double B, double gA) {
+  double v = fexp(gA), s = 0.0;
+  for (double y = A; y <= B; y += 1.0) {
+    s += v;
+    if (y < B) v *= ratio(P, y);
+  }
+  return s;
+}
+
+// sum_{y=A}^{B} p(y)/p(m) (oracle: hp_mass): exact within kK0 of the support
+// ends and for short windows, Euler-Maclaurin elsewhere
+__device__ __forceinline__ double wide_mass(const Pmf& P, double A, double B, double sd) {
+  const double N = P.N;
+  double tot = 0.0, A1 = A, B1 = B;
+  // up to three exact walks (left head, right head, or the whole short window):
+  // one evaluation site
+  for (int w = 0; w < 3; ++w) {
+    double ws = 0.0, we = -1.0;
+    if (w == 0 && A1 < kK0) {
+      ws = A1;
+      we = fmin(kK0 - 1.0, B);
+    } else if (w == 1 && B1 > N - kK0 && B1 >= A1) {
+      ws = fmax(N - kK0 + 1.0, A1);
+      we = B1;
+    } else if (w == 2 && B1 >= A1 && B1 - A1 < 32.0) {
+      ws = A1;
+      we = B1;
+    }
+    if (we >= ws) {
+      tot += walk_sum(P, ws, we, g_of(P, ws));
+      if (w == 0) A1 = we + 1.0;
+      else if (w == 1) B1 = ws - 1.0;
+      else B1 = A1 - 1.0;  // all summed
+    }
+  }
+  if (B1 < A1) return tot;
+  const double c = fmin(fmax(P.m, A1), B1);
+  double I = 0.0;
+  // parts [A1, c], [c, B1]; a part near both support ends splits at its midpoint
+  for (int pi = 0; pi < 4; ++pi) {
+    const int part = pi >> 1, sub = pi & 1;
+    const double u0 = part == 0 ? A1 : c, u1 = part == 0 ? c : B1;
     if (!(u1 > u0)) continue;
     const double L = u1 - u0;
-    const bool nl = (u0 + W.P.a) < L, nr = (W.P.N - u1 + W.P.b) < L;
+    const bool nl = (u0 + P.a) < L, nr = (N - u1 + P.b) < L;
     double a0 = u0, a1 = u1;
     bool snl = nl, snr = nr;
     if (nl && nr) {
-      const double cmid = 0.5 * (u0 + u1);
-      const double L2 = cmid - u0;
-      if (W.p_sub == 0) {
-        a1 = cmid;
-        snl = (u0 + W.P.a) < L2;
+      const double cm = 0.5 * (u0 + u1), L2 = cm - u0;
+      if (sub == 0) {
+        a1 = cm;
+        snl = (u0 + P.a) < L2;
         snr = false;
-      } else if (W.p_sub == 1) {
-        a0 = cmid;
-        snl = false;
-        snr = (W.P.N - u1 + W.P.b) < L2;
       } else {
-        continue;
+        a0 = cm;
+        snl = false;
+        snr = (N - u1 + P.b) < L2;
       }
-    } else if (W.p_sub > 0) {
+    } else if (sub == 1) {
       continue;
     }
-    W.p_u0 = a0;
-    W.p_u1 = a1;
-    W.p_nl = snl;
-    W.p_nr = snr;
-    if (snl || snr) {
-      W.p_v0 = snl ? flog(a0 + W.P.a) : flog(W.P.N - a1 + W.P.b);
-      W.p_v1 = snl ? flog(a1 + W.P.a) : flog(W.P.N - a0 + W.P.b);
-      const int k = (int)ceil((W.p_v1 - W.p_v0) / kLV);
-      W.p_k = k < 1 ? 1 : k;
+    const bool lg = snl || snr;
+    const double v0 = lg ? (snl ? flog(a0 + P.a) : flog(N - a1 + P.b)) : a0;
+    const double v1 = lg ? (snl ? flog(a1 + P.a) : flog(N - a0 + P.b)) : a1;
+    int k = lg ? (int)ceil((v1 - v0) / kLV) : (int)ceil((a1 - a0) / (kLX * sd));
+    k = k < 1 ? 1 : k;
+    const double dv = (v1 - v0) / k;
+    for (int j = 0; j < k; ++j) {
+      const double w0 = v0 + dv * j, w1 = v0 + dv * (j + 1);
+      const double h = 0.5 * (w1 - w0), cc = 0.5 * (w1 + w0);
+      double acc = 0.0;
+#pragma unroll MDFIT_HPDI_UNROLL
+      for (int i = 0; i < 6; ++i) {  // independent evaluations (ILP vs registers: MDFIT_HPDI_UNROLL)
+        const double gx = i < 3 ? -kGLX[2 - i] : kGLX[i - 3];
+        const double gw = kGLW[i < 3 ? 2 - i : i - 3];
+        const double v = cc + h * gx;
+        const double ev = lg ? fexp(v) : 1.0;
+        const double x = lg ? (snl ? ev - P.a : N + P.b - ev) : v;
+        acc += gw * ev * fexp(g_of(P, x));
+      }
+      I += h * acc;
+    }
+  }
+  // Euler-Maclaurin ends: one site for both
+  double fe[2], se[2];
+#pragma unroll 1
+  for (int e = 0; e < 2; ++e) {
+    double sx;
+    const double gx = gfun<true>(P, e == 0 ? A1 : B1, sx);
+    fe[e] = fexp(gx);
+    se[e] = sx;
+  }
+  return tot + I + 0.5 * (fe[0] + fe[1]) + (fe[1] * se[1] - fe[0] * se[0]) * (1.0 / 12.0);
+}
+
+// window [A, B] with absolute mass M -> the greedy's window (oracle: hp_fixup)
+__device__ __forceinline__ void wide_fixup(const Pmf& P, double A, double B, double M, double pA, double pB,
+                                           double& lo, double& hi) {
+  const double N = P.N;
+  double pl = A > 0.0 ? pA * rcp(ratio(P, A - 1.0)) : 0.0;
+  double pr = B < N ? pB * ratio(P, B) : 0.0;
+  for (int guard = 0; guard < (1 << 26); ++guard) {
+    if (M < kMass && (pl > 0.0 || pr > 0.0)) {  // grow
+      if (pl >= pr) {
+        A -= 1.0;
+        M += pl;
+        pA = pl;
+        pl = A > 0.0 ? pl * rcp(ratio(P, A - 1.0)) : 0.0;
+      } else {
+        B += 1.0;
+        M += pr;
+        pB = pr;
+        pr = B < N ? pr * ratio(P, B) : 0.0;
+      }
+      continue;
+    }
+    if (M < kMass) break;
+    const double pe = pB <= pA ? pB : pA;
+    if (A < B && M - pe >= kMass) {  // drop the less probable end
+      if (pB <= pA) {
+        M -= pB;
+        pr = pB;
+        B -= 1.0;
+        pB = pB * rcp(ratio(P, B));
+      } else {
+        M -= pA;
+        pl = pA;
+        A += 1.0;
+        pA = pA * ratio(P, A - 1.0);
+      }
+      continue;
+    }
+    const double pn = pl >= pr ? pl : pr;
+    if (!(pn > pe)) break;
+    if (pl >= pr) {  // slide toward the level set
+      A -= 1.0;
+      M += pl;
+      pA = pl;
+      pl = A > 0.0 ? pl * rcp(ratio(P, A - 1.0)) : 0.0;
     } else {
-      const int k = (int)ceil((a1 - a0) / (kLX * W.sd));
-      W.p_k = k < 1 ? 1 : k;
-    }
-    W.p_j = 0;
-    W.p_i = 0;
-    return true;
-  }
-  return false;
-}
-
-// next quadrature node of the current sub-part -> req_x (and the weight *
-// jacobian factor kept in p_h / p_cm); false when the part set is exhausted
-__device__ __forceinline__ double node_x(Wide& W, double& wj) {
-  const int i = W.p_i;
-  const double gx = i < 3 ? -kGLX[2 - i] : kGLX[i - 3];
-  const double gw = kGLW[i < 3 ? 2 - i : i - 3];
-  const int k = W.p_k, j = W.p_j;
-  if (W.p_nl || W.p_nr) {
-    const double w0 = W.p_v0 + (W.p_v1 - W.p_v0) * j / k, w1 = W.p_v0 + (W.p_v1 - W.p_v0) * (j + 1) / k;
-    const double h = 0.5 * (w1 - w0), c = 0.5 * (w1 + w0);
-    const double v = c + h * gx;
-    const double ev = exp(v);
-    wj = gw * h * ev;
-    return W.p_nl ? ev - W.P.a : W.P.N + W.P.b - ev;
-  }
-  const double L = W.p_u1 - W.p_u0;
-  const double w0 = W.p_u0 + L * j / k, w1 = W.p_u0 + L * (j + 1) / k;
-  const double h = 0.5 * (w1 - w0), c = 0.5 * (w1 + w0);
-  wj = gw * h;
-  return c + h * gx;
-}
-
-// Advance the machine (consuming the last evaluation when `have`) until it
-// requests the next one (returns true) or finishes (returns false).
-__device__ __forceinline__ bool wide_step(Wide& W, bool have) {
-  const double N = W.P.N, m = W.P.m;
-  for (int guard = 0; guard < 4096; ++guard) {
-    switch (W.phase) {
-      case W_G0:
-        if (!have) {
-          if (m > 0.0) { W.req_x = 0.0; W.req_s = 0; return true; }
-          W.g0 = 0.0;
-        } else {
-          W.g0 = W.res_g;
-          have = false;
-        }
-        W.phase = W_GN;
-        break;
-      case W_GN:
-        if (!have) {
-          if (m < N) { W.req_x = N; W.req_s = 0; return true; }
-          W.gN = 0.0;
-        } else {
-          W.gN = W.res_g;
-          have = false;
-        }
-        W.phase = W_DECIDE;
-        break;
-      case W_DECIDE:
-        W.t = kT0;
-        {
-          const bool L0 = m == 0.0 || W.g0 >= W.t, R0 = m == N || W.gN >= W.t;
-          W.one = (L0 && !R0) ? 0 : ((R0 && !L0) ? 1 : -1);
-        }
-        W.it = 0;
-        if (W.one >= 0) {
-          W.x = W.one == 0 ? fmax(W.mu, m + 1.0) : fmin(W.mu, m - 1.0);
-          W.lb = W.one == 0 ? m : 0.0;
-          W.hb = W.one == 0 ? N : m;
-          W.phase = W_ONE_TOP;
-        } else {
-          W.tL = -INFINITY;
-          W.tH = 0.0;
-          W.xl = m - W.sd;
-          W.xr = m + W.sd;
-          W.phase = W_TWO_TOP;
-        }
-        break;
-      // ---------------- one-sided: window [0, B] or [A, N] ----------------
-      case W_ONE_TOP:
-        W.A = W.one == 0 ? 0.0 : ceil(W.x);
-        W.B = W.one == 0 ? floor(W.x) : N;
-        W.m_ret = W_ONE_FX;
-        W.phase = W_MASS_BEGIN;
-        break;
-      case W_ONE_FX:
-        if (!have) {
-          W.M = W.M * W.P.pm;  // mass() result (relative) -> absolute
-          W.req_x = W.x;
-          W.req_s = 0;
-          return true;
-        } else {
-          have = false;
-          const double fx = exp(W.res_g) * W.P.pm;
-          const double Md = W.M;
-          const double F = log(Md / (1.0 - Md)) - log(kMass / (1.0 - kMass));
-          const double jac = W.one == 0 ? W.x + W.P.a : N - W.x + W.P.b;
-          const double dF = fx * jac * (1.0 / Md + 1.0 / (1.0 - Md));
-          double xn;
-          if (W.one == 0) {
-            if (F > 0.0) W.hb = W.x;
-            else W.lb = W.x;
-            xn = exp(log(W.x + W.P.a) - F / dF) - W.P.a;
-          } else {
-            if (F > 0.0) W.lb = W.x;
-            else W.hb = W.x;
-            xn = N + W.P.b - exp(log(N - W.x + W.P.b) - F / dF);
-          }
-          if (!(W.lb < xn && xn < W.hb)) xn = 0.5 * (W.lb + W.hb);
-          if (fabs(xn - W.x) < fmax(kStop, 2e-5 * W.x) || W.it >= 40) {
-            W.phase = W_FIX_A;
-          } else {
-            W.x = xn;
-            W.it += 1;
-            W.phase = W_ONE_TOP;
-          }
-        }
-        break;
-      // ---------------- two-sided: level-set Newton ------------------------
-      case W_TWO_TOP:
-        if (m == 0.0 || W.g0 >= W.t) {
-          W.xl = 0.0;
-          W.cl = 1;
-          W.phase = W_TWO_ROOTR;
-        } else {
-          W.cl = 0;
-          W.r_lo = 0.0;
-          W.r_hi = m;
-          W.r_x = fmin(fmax(W.xl, 0.0), m);
-          W.r_rising = 1;
-          W.r_it = 0;
-          W.r_ret = W_TWO_ROOTR;
-          W.phase = W_ROOT;
-        }
-        break;
-      case W_TWO_ROOTR:
-        if (!W.cl) W.xl = W.r_x;  // the left root (when it ran)
-        if (m == N || W.gN >= W.t) {
-          W.xr = N;
-          W.cr = 1;
-          W.phase = W_TWO_MASS;
-        } else {
-          W.cr = 0;
-          W.r_lo = m;
-          W.r_hi = N;
-          W.r_x = fmin(fmax(W.xr, m), N);
-          W.r_rising = 0;
-          W.r_it = 0;
-          W.r_ret = W_TWO_MASS;
-          W.phase = W_ROOT;
-        }
-        break;
-      case W_TWO_MASS:
-        if (!W.cr) W.xr = W.r_x;
-        W.A = ceil(W.xl);
-        W.B = floor(W.xr);
-        W.m_ret = W_TWO_SL;
-        W.phase = W_MASS_BEGIN;
-        break;
-      case W_TWO_SL:
-        if (!have) {
-          W.M = W.M * W.P.pm;
-          if (W.M >= kMass) W.tL = W.t;
-          else W.tH = W.t;
-          W.Dp = 0.0;
-          W.mv = 0.0;
-          if (!W.cl) { W.req_x = W.xl; W.req_s = 1; return true; }
-        } else {
-          have = false;
-          const double sl = W.res_s;
-          W.Dp += exp(W.t) / sl;
-          W.mv += 1.0 / sl;
-        }
-        W.phase = W_TWO_SR;
-        break;
-      case W_TWO_SR:
-        if (!have) {
-          if (!W.cr) { W.req_x = W.xr; W.req_s = 1; return true; }
-        } else {
-          have = false;
-          const double sr = -W.res_s;
-          W.Dp += exp(W.t) / sr;
-          W.mv += 1.0 / sr;
-        }
-        {
-          W.Dp *= W.P.pm;
-          bool stop = W.it >= 40;
-          if (!stop) {
-            double tn;
-            if (W.Dp > 0.0) {
-              const double dt = (log(W.M) - log(kMass)) * W.M / W.Dp;
-              stop = fabs(dt) * W.mv < fmax(kStop, 2e-5 * W.A);
-              tn = W.t + dt;
-            } else {
-              tn = 0.5 * (W.tL + W.tH);  // both ends clamped: raise the level
-            }
-            if (!stop) {
-              if (!(W.tL < tn && tn < W.tH)) tn = W.tL > -INFINITY ? 0.5 * (W.tL + W.tH) : W.t - fmax(1.0, fabs(W.t));
-              W.t = tn;
-              W.it += 1;
-            }
-          }
-          W.phase = stop ? W_FIX_A : W_TWO_TOP;
-        }
-        break;
-      // ---------------- root sub-machine: g(x) = t on [r_lo, r_hi] ---------
-      case W_ROOT:
-        if (!have) {
-          W.req_x = W.r_x;
-          W.req_s = 1;
-          return true;
-        } else {
-          have = false;
-          const double gx = W.res_g - W.t;
-          if (fabs(gx) < 1e-12) {
-            W.phase = W.r_ret;
-            break;
-          }
-          if ((gx < 0.0) == (W.r_rising != 0)) W.r_lo = W.r_x;
-          else W.r_hi = W.r_x;
-          const double sx = W.res_s;
-          double xn = sx != 0.0 ? W.r_x - gx / sx : 0.5 * (W.r_lo + W.r_hi);
-          if (!(W.r_lo < xn && xn < W.r_hi)) xn = 0.5 * (W.r_lo + W.r_hi);
-          const bool conv = fabs(xn - W.r_x) < 0.05;
-          W.r_x = xn;
-          W.r_it += 1;
-          if (conv || W.r_it >= 60) W.phase = W.r_ret;
-        }
-        break;
-      // ---------------- mass sub-machine: sum_{A..B} p / p(m) ---------------
-      case W_MASS_BEGIN:
-        W.m_tot = 0.0;
-        W.m_A1 = W.A;
-        W.m_B1 = W.B;
-        if (W.m_A1 < kK0) {
-          W.m_e = fmin(kK0 - 1.0, W.B);
-          W.ew_y = W.m_A1;
-          W.ew_end = W.m_e;
-          W.ew_ret = W_MASS_HR;
-          W.m_mode = 1;  // A1 <- e + 1 on return
-          W.phase = W_EXACT_WALK;
-        } else {
-          W.m_mode = 0;
-          W.phase = W_MASS_HR;
-        }
-        break;
-      case W_MASS_HR:
-        if (W.m_mode == 1) {
-          W.m_A1 = W.m_e + 1.0;
-          W.m_mode = 0;
-        }
-        if (W.m_mode == 2) {  // back from the right head
-          W.m_B1 = W.m_e - 1.0;
-          W.m_mode = 0;
-          W.phase = W_MASS_MID;
-          break;
-        }
-        if (W.m_B1 > N - kK0 && W.m_B1 >= W.m_A1) {
-          W.m_e = fmax(N - kK0 + 1.0, W.m_A1);
-          W.ew_y = W.m_e;
-          W.ew_end = W.m_B1;
-          W.ew_ret = W_MASS_HR;
-          W.m_mode = 2;
-          W.phase = W_EXACT_WALK;
-        } else {
-          W.phase = W_MASS_MID;
-        }
-        break;
-      case W_MASS_MID:
-        if (W.m_mode == 3) {  // back from the short-window exact sum
-          W.m_mode = 0;
-          W.M = W.m_tot;
-          W.phase = W.m_ret;
-          break;
-        }
-        if (W.m_B1 < W.m_A1) {
-          W.M = W.m_tot;
-          W.phase = W.m_ret;
-          break;
-        }
-        if (W.m_B1 - W.m_A1 < 32.0) {
-          W.ew_y = W.m_A1;
-          W.ew_end = W.m_B1;
-          W.ew_ret = W_MASS_MID;
-          W.m_mode = 3;
-          W.phase = W_EXACT_WALK;
-          break;
-        }
-        W.m_c = fmin(fmax(m, W.m_A1), W.m_B1);
-        W.m_I = 0.0;
-        W.p_part = 0;
-        W.p_sub = 0;
-        W.phase = part_setup(W) ? W_MASS_NODES : W_MASS_ENDA;
-        break;
-      case W_MASS_NODES: {
-        double wj;
-        if (!have) {
-          W.req_x = node_x(W, wj);
-          W.req_s = 0;
-          return true;
-        }
-        have = false;
-        (void)node_x(W, wj);
-        W.m_I += wj * exp(W.res_g);
-        if (++W.p_i == 6) {
-          W.p_i = 0;
-          if (++W.p_j == W.p_k) {
-            ++W.p_sub;
-            if (!part_setup(W)) W.phase = W_MASS_ENDA;
-          }
-        }
-        break;
-      }
-      case W_MASS_ENDA:
-        if (!have) {
-          W.req_x = W.m_A1;
-          W.req_s = 1;
-          return true;
-        }
-        have = false;
-        W.fA = exp(W.res_g);
-        W.sA = W.res_s;
-        W.phase = W_MASS_ENDB;
-        break;
-      case W_MASS_ENDB:
-        if (!have) {
-          W.req_x = W.m_B1;
-          W.req_s = 1;
-          return true;
-        }
-        have = false;
-        {
-          const double fB = exp(W.res_g), sB = W.res_s;
-          W.M = W.m_tot + W.m_I + 0.5 * (W.fA + fB) + (fB * sB - W.fA * W.sA) * (1.0 / 12.0);
-        }
-        W.phase = W.m_ret;
-        break;
-      // ---------------- exact walk: m_tot += sum_{ew_y..ew_end} p/p(m) -------
-      case W_EXACT_WALK:
-        if (!have) {
-          W.req_x = W.ew_y;
-          W.req_s = 0;
-          return true;
-        }
-        have = false;
-        {
-          double v = exp(W.res_g), s = 0.0;
-          for (double y = W.ew_y; y <= W.ew_end; y += 1.0) {
-            s += v;
-            if (y < W.ew_end) v *= ratio(W.P, y);
-          }
-          W.m_tot += s;
-        }
-        W.phase = W.ew_ret;
-        break;
-      // ---------------- fix-up (oracle: hp_fixup) ----------------------------
-      case W_FIX_A:
-        if (!have) {
-          W.req_x = W.A;
-          W.req_s = 0;
-          return true;
-        }
-        have = false;
-        W.pA = exp(W.res_g) * W.P.pm;
-        W.pB = W.pA;
-        W.phase = W_FIX_B;
-        break;
-      case W_FIX_B:
-        if (!have) {
-          if (W.B != W.A) {
-            W.req_x = W.B;
-            W.req_s = 0;
-            return true;
-          }
-        } else {
-          have = false;
-          W.pB = exp(W.res_g) * W.P.pm;
-        }
-        W.pl = W.A > 0.0 ? W.pA * rcp(ratio(W.P, W.A - 1.0)) : 0.0;
-        W.pr = W.B < N ? W.pB * ratio(W.P, W.B) : 0.0;
-        W.phase = W_FIX_WALK;
-        break;
-      case W_FIX_WALK: {
-        double A = W.A, B = W.B, M = W.M, pA = W.pA, pB = W.pB, pl = W.pl, pr = W.pr;
-        while (M < kMass && (pl > 0.0 || pr > 0.0)) {
-          if (pl >= pr) {
-            A -= 1.0;
-            M += pl;
-            pA = pl;
-            pl = A > 0.0 ? pl * rcp(ratio(W.P, A - 1.0)) : 0.0;
-          } else {
-            B += 1.0;
-            M += pr;
-            pB = pr;
-            pr = B < N ? pr * ratio(W.P, B) : 0.0;
-          }
-        }
-        for (int g2 = 0; g2 < (1 << 24); ++g2) {
-          const double pe = pB <= pA ? pB : pA;
-          if (A < B && M - pe >= kMass) {
-            if (pB <= pA) {
-              M -= pB;
-              pr = pB;
-              B -= 1.0;
-              pB = pB * rcp(ratio(W.P, B));
-            } else {
-              M -= pA;
-              pl = pA;
-              A += 1.0;
-              pA = pA * ratio(W.P, A - 1.0);
-            }
-            continue;
-          }
-          const double pn = pl >= pr ? pl : pr;
-          if (pn > pe) {
-            if (pl >= pr) {
-              A -= 1.0;
-              M += pl;
-              pA = pl;
-              pl = A > 0.0 ? pl * rcp(ratio(W.P, A - 1.0)) : 0.0;
-            } else {
-              B += 1.0;
-              M += pr;
-              pB = pr;
-              pr = B < N ? pr * ratio(W.P, B) : 0.0;
-            }
-            continue;
-          }
-          break;
-        }
-        W.A = A;
-        W.B = B;
-        W.phase = W_DONE;
-        return false;
-      }
-      case W_DONE:
-      default:
-        return false;
+      B += 1.0;
+      M += pr;
+      pB = pr;
+      pr = B < N ? pr * ratio(P, B) : 0.0;
     }
   }
-  W.phase = W_DONE;  // (unreachable: a guard against a logic error looping)
-  return false;
+  lo = A;
+  hi = B;
+}
+
+__device__ __forceinline__ void wide_window(const WideRec& r, double& lo, double& hi) {
+  Pmf P;
+  load_pmf(P, r);
+  const double N = P.N, m = P.m, sd = r.sd, mu = r.mu;
+  double gE[2];
+#pragma unroll 1
+  for (int e = 0; e < 2; ++e) {  // g(0), g(N): one site
+    const bool need = e == 0 ? m > 0.0 : m < N;
+    gE[e] = need ? g_of(P, e == 0 ? 0.0 : N) : 0.0;
+  }
+  const double g0 = gE[0], gN = gE[1];
+  double t = kT0;
+  const bool L0 = m == 0.0 || g0 >= t, R0 = m == N || gN >= t;
+  const int one = (L0 && !R0) ? 0 : ((R0 && !L0) ? 1 : -1);
+  double x = one == 0 ? fmax(mu, m + 1.0) : fmin(mu, m - 1.0);
+  double lb = one == 0 ? m : 0.0, hb = one == 0 ? N : m;
+  double tL = -INFINITY, tH = 0.0;
+  double xe[2] = {m - sd, m + sd};  // two-sided ends
+  double A = m, B = m, M = P.pm;
+  for (int it = 0;; ++it) {
+    bool cl = false, cr = false;
+    if (one < 0) {
+      cl = m == 0.0 || g0 >= t;
+      cr = m == N || gN >= t;
+      // the free ends' roots of g = t (oracle: hp_root): one site for both
+#pragma unroll 1
+      for (int e = 0; e < 2; ++e) {
+        const bool clamped = e == 0 ? cl : cr;
+        if (clamped) {
+          xe[e] = e == 0 ? 0.0 : N;
+          continue;
+        }
+        double rlo = e == 0 ? 0.0 : m, rhi = e == 0 ? m : N;
+        const bool rising = e == 0;
+        double xr = fmin(fmax(xe[e], rlo), rhi);
+        for (int k = 0; k < 60; ++k) {
+          double sx;
+          const double gx = gfun<true>(P, xr, sx) - t;
+          if (fabs(gx) < 1e-12) break;
+          if ((gx < 0.0) == rising) rlo = xr;
+          else rhi = xr;
+          double xn = sx != 0.0 ? xr - gx / sx : 0.5 * (rlo + rhi);
+          if (!(rlo < xn && xn < rhi)) xn = 0.5 * (rlo + rhi);
+          const bool conv = fabs(xn - xr) < 0.05;
+          xr = xn;
+          if (conv) break;
+        }
+        xe[e] = xr;
+      }
+      A = ceil(xe[0]);
+      B = floor(xe[1]);
+    } else {
+      A = one == 0 ? 0.0 : ceil(x);
+      B = one == 0 ? floor(x) : N;
+    }
+    M = wide_mass(P, A, B, sd) * P.pm;
+    // the evaluations after the mass: f(x) (one-sided) or s at the two ends
+    double pe[2] = {0.0, 0.0};
+#pragma unroll 1
+    for (int e = 0; e < 2; ++e) {
+      const bool need = one >= 0 ? e == 0 : (e == 0 ? !cl : !cr);
+      if (!need) continue;
+      double sx;
+      const double gx = gfun<true>(P, one >= 0 ? x : xe[e], sx);
+      pe[e] = one >= 0 ? fexp(gx) * P.pm : sx;
+    }
+    if (one >= 0) {
+      const double fx = pe[0];
+      const double F = log(M / (1.0 - M)) - log(kMass / (1.0 - kMass));
+      const double jac = one == 0 ? x + P.a : N - x + P.b;
+      const double dF = fx * jac * (1.0 / M + 1.0 / (1.0 - M));
+      double xn;
+      if (one == 0) {
+        if (F > 0.0) hb = x;
+        else lb = x;
+        xn = exp(log(x + P.a) - F / dF) - P.a;
+      } else {
+        if (F > 0.0) lb = x;
+        else hb = x;
+        xn = N + P.b - exp(log(N - x + P.b) - F / dF);
+      }
+      if (!(lb < xn && xn < hb)) xn = 0.5 * (lb + hb);
+      if (fabs(xn - x) < fmax(kStop, 2e-5 * x) || it >= 40) break;
+      x = xn;
+    } else {
+      if (M >= kMass) tL = t;
+      else tH = t;
+      double Dp = 0.0, mv = 0.0;
+      if (!cl) {
+        Dp += exp(t) / pe[0];
+        mv += 1.0 / pe[0];
+      }
+      if (!cr) {
+        Dp += exp(t) / -pe[1];
+        mv += 1.0 / -pe[1];
+      }
+      Dp *= P.pm;
+      if (it >= 40) break;
+      double tn;
+      if (Dp > 0.0) {
+        const double dt = (log(M) - log(kMass)) * M / Dp;
+        if (fabs(dt) * mv < fmax(kStop, 2e-5 * A)) break;
+        tn = t + dt;
+      } else {
+        tn = 0.5 * (tL + tH);  // both ends clamped: raise the level
+      }
+      if (!(tL < tn && tn < tH)) tn = tL > -INFINITY ? 0.5 * (tL + tH) : t - fmax(1.0, fabs(t));
+      t = tn;
+    }
+  }
+  // the fix-up from the end pmfs (one site for both)
+  double pAB[2];
+#pragma unroll 1
+  for (int e = 0; e < 2; ++e) {
+    const bool need = e == 0 || B != A;
+    pAB[e] = need ? fexp(g_of(P, e == 0 ? A : B)) * P.pm : pAB[0];
+  }
+  wide_fixup(P, A, B, M, pAB[0], pAB[1], lo, hi);
 }
 
 }  // namespace hpdi

@@ -65,6 +65,32 @@ __device__ __forceinline__ double flog1p(double x) {
   return um1 == 0.0 ? x : flog(u) * (x * rcp(um1));
 }
 
+// exp(x), ~1 ulp: x = n ln2 + r (Cody-Waite, |r| <= ln2/2), e^r by a degree-12
+// Taylor polynomial (|error| < 2e-17 on that range), 2^n by ldexp.  Saturates
+// to 0 / +inf outside [-745, 709.8]; NaN passes through.
+__device__ __forceinline__ double fexp(double x) {
+  constexpr double kLog2e = 1.4426950408889634074;
+  constexpr double kLn2Hi = 6.93147180369123816490e-01;
+  constexpr double kLn2Lo = 1.90821492927058770002e-10;
+  const double n = rint(x * kLog2e);
+  const double r = fma(-n, kLn2Lo, fma(-n, kLn2Hi, x));
+  double p = 1.0 / 479001600.0;
+  p = fma(p, r, 1.0 / 39916800.0);
+  p = fma(p, r, 1.0 / 3628800.0);
+  p = fma(p, r, 1.0 / 362880.0);
+  p = fma(p, r, 1.0 / 40320.0);
+  p = fma(p, r, 1.0 / 5040.0);
+  p = fma(p, r, 1.0 / 720.0);
+  p = fma(p, r, 1.0 / 120.0);
+  p = fma(p, r, 1.0 / 24.0);
+  p = fma(p, r, 1.0 / 6.0);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  const double y = __builtin_amdgcn_ldexp(p, (int)fmax(fmin(n, 1100.0), -1100.0));
+  return x < -745.2 ? 0.0 : (x > 709.8 ? INFINITY : y);
+}
+
 struct LG3 {
   double l;  // lnGamma(x)
   double p;  // digamma(x)

