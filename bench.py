@@ -1,28 +1,38 @@
-"""Benchmark: TaxID damage fits/s of the MI355X MAP fit engine (BASELINE.json metric).
+"""Benchmark: TaxID damage fits/s of the MI355X fit engine (BASELINE.json metric).
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[1]): 10,000 synthetic TaxIDs
-per GPU x 30 positions (z = +-1..15), seed 1 (+ rank), MAP beta-binomial fit of
+N = 1 (the headline, BASELINE.json configs[1]): 10,000
+synthetic TaxIDs x 30 positions (z = +-1..15), seed 1, MAP beta-binomial fit of
 model_PMD and model_null on all / forward / reverse positions (the 6 sub-fits
 the reference runs per TaxID, fits.py:438-439, 311-313, 333-335), the record
-assembly, noise estimates and per-position predictions.  One step = one
-mdfit_fit_batch launch over the rank's shard with inputs already resident in HBM,
-plus (N > 1) the single RCCL gather of the packed result records to rank 0
-(asynchronous, overlapping the next step's fit; every gather has completed
-before the clock stops).
-Weak scaling: every rank fits its own 10,000 taxa.
+assembly, noise estimates, per-position predictive medians and the exact 68 %
+predictive HPDI.  One step = one mdfit_fit_batch launch with inputs resident in
+HBM.
+
+N > 1 (configs[3], C4): 1,000,000 TaxIDs in total, strong scaling: rank r fits
+its contiguous 1M/N shard (synthetic, seed 3 + 1000 r) and every step ends with
+the ONE RCCL gather of the packed result records to rank 0 (synchronous, inside
+the timed region; no step overlaps another).
 
 Printed JSON (rank 0): the driver contract fields plus
-  roofline          HBM roofline of the fit kernel (algorithmic bytes / kernel
-                    time, HIP events on the launch stream; traffic from the
-                    committed rocprofv3 PMC pass, profiles/)
+  roofline          HBM roofline of the dominant kernel (fit_kernel): SURVEY.md
+                    §8(d)'s algorithmic 448 B/taxon / kernel time (HIP events
+                    on the launch stream); PMC traffic from profiles/;
+                    hbm_intermediate: the 816 B/taxon the kernel actually moves
+                    (the K0 -> K1 -> K3 hand-off through the record)
   compute_roofline  useful point-evaluations/s vs the register-only probe of the
                     same point evaluation (the kernel's real bound: FP64 VALU)
-  cpu_baseline      the CPU oracle (C/OpenMP restatement of the same fit,
-                    oracle/mdfit_oracle.c) on the same 10k-taxon workload
+  host_to_host      (N = 1) the product call from pinned host buffers: H2D of
+                    y, N (+ the mismatch counts), the fit, D2H of the 32 record
+                    columns, predictions and status
+  cpu_baseline      (N = 1) the CPU oracle (C/OpenMP restatement of the same
+                    fit) on the box's core share, median of 5 over the whole
+                    workload, with the reference-dispatch-shape figure beside
+                    it (tools/cpu_reference_dispatch.py: scipy per taxon, a Pool
+                    per 1,000-taxon chunk as fits.py:692-706)
 """
 
 from __future__ import annotations
@@ -40,13 +50,16 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 TAXA_PER_GPU = 10_000
+C4_TAXA = 1_000_000
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-# algorithmic bytes per taxon:
-#  whole call: y,N 2x30x4 + mismatch 30x12x4 in, 25 result fields x8 +
-#              predictions 3x30x4 + status 4 out
-#  fit_kernel: y,N 2x30x4 + 6 initial points 6x4x8 in, 6 sub-fit records 6x8x8 out
-CALL_BYTES_PER_TAXON = 240 + 1440 + 200 + 360 + 4
+# bytes per taxon:
+#  algorithmic: y,N 2x30x4 in + 26 numeric result fields x8 out
+#  fit_kernel as built: y,N 2x30x4 + 6 initial points 6x4x8 in, 6 sub-fit records 6x8x8 out
+#  whole call: y,N + mismatch 30x12x4 in, 25 result fields x8 + predictions
+#              3x30x4 + status 4 out
+ALG_BYTES_PER_TAXON = 240 + 208
 FIT_BYTES_PER_TAXON = 240 + 192 + 384
+CALL_BYTES_PER_TAXON = 240 + 1440 + 200 + 360 + 4
 NPTS = np.array([30, 30, 15, 15, 15, 15])
 
 
@@ -59,7 +72,9 @@ def parse():
     ap.add_argument("--mode", choices=["map", "nuts"], default="map",
                     help="map: config C2 (the headline); nuts: config C3, the reference's sampler")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the process's core share (affinity, OMP_NUM_THREADS)")
+    ap.add_argument("--workload", choices=["c2", "c4"], default=None,
+                    help="default: c2 at N = 1 (the headline), c4 (1M taxa, strong scaling) at N > 1")
     a = ap.parse_args()
     if a.steps is None:
         a.steps = 20 if a.mode == "map" else 1
@@ -82,15 +97,32 @@ def pmc_traffic(kernel: str = "fit_kernel", taxa: int = TAXA_PER_GPU):
         return None
 
 
+def host_cores() -> tuple[int, int]:
+    """(threads to use, CPUs visible): the process's affinity set, capped by
+    OMP_NUM_THREADS when the box sets it (its CPU share for one GPU)."""
+    try:
+        visible = len(os.sched_getaffinity(0))
+    except AttributeError:
+        visible = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(visible, share) if share > 0 else visible), (os.cpu_count() or visible)
+
+
+def ref_dispatch_baseline(cores: int, taxa: int = 500) -> dict | None:
+    """tools/cpu_reference_dispatch.py in a child process, started before this
+    process touches the GPU (its Pool forks workers)."""
+    import subprocess
+
+    try:
+        r = subprocess.run([sys.executable, str(ROOT / "tools" / "cpu_reference_dispatch.py"), "--taxa", str(taxa),
+                            "--cores", str(cores)], capture_output=True, text=True, timeout=600, check=True)
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:  # reported, never fatal: the headline does not depend on it
+        return {"error": repr(e)[:200]}
+
+
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
-    from metadamage_amd import _lib, engine
-    from metadamage_amd.distributed import alloc_records, gather_records
-    from metadamage_amd.synthetic import generate
-
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -98,51 +130,52 @@ def main():
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    nuts = args.mode == "nuts"
+    workload = args.workload or ("c4" if world > 1 and not nuts else "c2")
+    cores, visible = host_cores()
+    if args.cpu_threads > 0:
+        cores = args.cpu_threads
+    ref_dispatch = None
+    if not args.no_cpu_baseline and world == 1 and not nuts:
+        ref_dispatch = ref_dispatch_baseline(cores)  # before any GPU call
+
+    import torch
+    import torch.distributed as dist
+
+    from metadamage_amd import _lib, engine
+    from metadamage_amd.distributed import alloc_records, gather_records, shard_capacity, shard_range
+    from metadamage_amd.synthetic import generate
+
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
     # ---- synthetic shard, resident in HBM before timing -------------------
-    nuts = args.mode == "nuts"
-    T = args.taxa or (100_000 if nuts else TAXA_PER_GPU)
-    b = generate(T, seed=(2 if nuts else 1) + rank)  # C2 seed 1, C3 seed 2
+    if workload == "c4":
+        lo, hi = shard_range(C4_TAXA, rank, world)
+        T, cap, seed, total_per_step = hi - lo, shard_capacity(C4_TAXA, world), 3 + 1000 * rank, C4_TAXA
+    else:
+        T = args.taxa or (100_000 if nuts else TAXA_PER_GPU)
+        lo, cap, seed, total_per_step = rank * T, T, (2 if nuts else 1) + rank, T * world
+    b = generate(T, seed=seed)  # C2 seed 1, C3 seed 2, C4 seed 3
     ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm, device=dev)
-    # N > 1: two record sets, so the gather of step i (async, on the backend's
-    # stream) overlaps the fit of step i+1; a set is refilled only after its
-    # previous gather has been waited for (the way a multi-batch run overlaps
-    # its exchange with the next batch's fit)
-    recs = [alloc_records(T, dev) for _ in range(2 if world > 1 and not nuts else 1)]
-    fbs = [engine.FitBatch(r.out, r.pred, r.status) for r in recs]
-    pending = [None] * len(recs)
-    opts = _lib.default_opts(mode=_lib.MODE_NUTS if nuts else _lib.MODE_MAP, index_base=rank * T)
+    rec = alloc_records(cap, dev)
+    fb = engine.FitBatch(rec.out[:T], rec.pred[:T], rec.status[:T])
+    opts = _lib.default_opts(mode=_lib.MODE_NUTS if nuts else _lib.MODE_MAP, index_base=lo)
     stream = torch.cuda.current_stream(dev)
-    n_step = [0]
 
     def step():
-        k = n_step[0] % len(recs)
-        n_step[0] += 1
-        if pending[k] is not None:
-            pending[k].wait()
-            pending[k] = None
-        engine.fit_batch_device(ty, tN, tm, opts, fbs[k], stream=stream)
-        if world > 1:
-            _, pending[k] = gather_records(recs[k].stage(), T, rank, world, async_op=True)
-
-    def drain():
-        for k, w in enumerate(pending):
-            if w is not None:
-                w.wait()
-                pending[k] = None
+        engine.fit_batch_device(ty, tN, tm, opts, fb, stream=stream)
+        if world > 1:  # the one gather of the packed records to rank 0 (synchronous)
+            buf = rec.stage()
+            gather_records(buf, cap, rank, world)
 
     for _ in range(args.warmup):
         step()
-    drain()
     torch.cuda.synchronize(dev)
     # HIP events on the launch stream, recorded by the library around
-    # fit_kernel only (torch events see only torch's stream; two more events
-    # per call around the whole call cost ~1.5 % of the step, so the call time
-    # is the step time)
+    # fit_kernel only (torch events see only torch's stream)
     engine.profile_enable(True, fit_only=True)
     if world > 1:
         dist.barrier()
@@ -150,7 +183,6 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step()
-    drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -160,15 +192,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     _, fit_ms_sum, n_calls = engine.profile_read()
-    call_ms_sum = elapsed * 1e3 / args.steps * n_calls  # the step (one call + its gather) by the wall clock
+    call_ms_sum = elapsed * 1e3 / args.steps * n_calls  # the step by the wall clock
     engine.profile_enable(False)
     assert n_calls == min(args.steps, 256), (n_calls, args.steps)  # the library keeps up to 256 calls
 
-    # per-rank diagnostics of the last step
-    last = recs[(n_step[0] - 1) % len(recs)]
-    res, out, status = fbs[(n_step[0] - 1) % len(recs)], last.out, last.status
-    o = out.cpu().numpy()
-    st = status.cpu().numpy()
+    o = fb.out.cpu().numpy()
+    st = fb.status.cpu().numpy()
     evals = o[:, _lib.F_DIAG + 5 :: _lib.DIAG_STRIDE][:, :6]
     useful_pe = float((evals * NPTS).sum())
     # position slots the fit kernel's 32-lane groups spent: an all-position fit
@@ -177,15 +206,14 @@ def main():
     slot_pe = float(30 * group_evals.sum())
 
     if rank == 0 and nuts:
-        smp = engine.samples_view(res, T, opts)[:64].cpu().numpy()
+        smp = engine.samples_view(fb, T, opts)[:64].cpu().numpy()
         print(json.dumps(nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, b, smp)),
               flush=True)
     elif rank == 0:
-        total = T * world * args.steps
-        value = total / elapsed
+        value = total_per_step * args.steps / elapsed
         k_avg_s = fit_ms_sum / n_calls / 1e3
         call_avg_s = call_ms_sum / n_calls / 1e3
-        achieved = FIT_BYTES_PER_TAXON * T / k_avg_s / 1e9
+        achieved = ALG_BYTES_PER_TAXON * T / k_avg_s / 1e9
         traffic = pmc_traffic("fit_kernel", T)
         # compute roofline: register-only probe of the same point evaluation
         n_waves, iters = 256 * 16, 64
@@ -198,6 +226,14 @@ def main():
         torch.cuda.synchronize(dev)
         probe_rate = 3 * n_waves * 60 * iters / (e0.elapsed_time(e1) / 1e3)  # 60 points per wave-iteration
         useful_rate = useful_pe / k_avg_s
+        if workload == "c4":
+            wl = (f"C4: 1M synthetic TaxIDs x +-15 positions sharded over {world} GPUs ({T} on rank 0), MAP "
+                  "beta-binomial damage fit (6 sub-fits per TaxID) + record assembly + predictive HPDI, then one "
+                  "RCCL gather of the packed fit records to rank 0 per step")
+        else:
+            wl = ("C2: 10k synthetic TaxIDs x +-15 positions per GPU, MAP beta-binomial damage fit "
+                  "(model_PMD + model_null on all/forward/reverse = 6 sub-fits per TaxID) + record assembly + "
+                  "exact 68 % predictive HPDI")
         line = {
             "metric": "TaxID damage fits/sec",
             "value": round(value, 1),
@@ -207,13 +243,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if workload == "c4" else "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (SURVEY.md §8(d) generator, seed 1+rank)",
+            "data": "synthetic (SURVEY.md §8(d) generator; " + ("C4 seed 3 + 1000 x rank per shard)" if workload == "c4"
+                                                                    else "C2 seed 1 + rank)"),
             "config": {
-                "workload": "C2: 10k synthetic TaxIDs x +-15 positions per GPU, MAP beta-binomial damage fit "
-                "(model_PMD + model_null on all/forward/reverse = 6 sub-fits per TaxID) + record assembly",
+                "workload": wl,
+                "taxa_total": total_per_step,
                 "taxa_per_gpu": T,
                 "positions": 30,
                 "parallelism": f"taxon-shard x{world}" + (" + RCCL gather" if world > 1 else ""),
@@ -226,10 +263,17 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "kernel": "fit_kernel",
-                "note": "HBM fraction is structural (816 B per taxon against ~1e3 FP64 point evaluations); "
-                "the kernel is FP64-VALU / latency bound: see compute_roofline (SURVEY.md 8(d), DESIGN.md 4)",
+                "bytes_per_taxon": ALG_BYTES_PER_TAXON,
+                "note": "algorithmic bytes per SURVEY.md 8(d) (y,N in + 26 result fields out = 448 B/taxon); the "
+                "HBM fraction is structural (~1e3 FP64 point evaluations per taxon): the kernel is FP64-VALU / "
+                "latency bound, see compute_roofline (DESIGN.md 4)",
                 "kernel_ms_avg": round(k_avg_s * 1e3, 4),
-                "bytes_per_taxon": FIT_BYTES_PER_TAXON,
+                "hbm_intermediate": {
+                    "bytes_per_taxon": FIT_BYTES_PER_TAXON,
+                    "achieved": round(FIT_BYTES_PER_TAXON * T / k_avg_s / 1e9, 3),
+                    "note": "what the kernel moves as built: y,N + the 6 initial points in, the 6 sub-fit records "
+                    "out (the K0 -> K1 -> K3 hand-off through the record)",
+                },
                 "call_ms_avg": round(call_avg_s * 1e3, 4),
                 "call_bytes_per_taxon": CALL_BYTES_PER_TAXON,
                 "call_achieved": round(CALL_BYTES_PER_TAXON * T / call_avg_s / 1e9, 3),
@@ -245,13 +289,49 @@ def main():
             },
             "status_ok_frac": float((st == 0).mean()),
         }
+        if world == 1:
+            line["host_to_host"] = host_to_host(engine, b, opts, dev, max(5, args.steps // 2))
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure
-            line["cpu_baseline"], ref = cpu_baseline(b, args.cpu_threads)
+            line["cpu_baseline"], ref = cpu_baseline(b, cores, visible)
+            if ref_dispatch is not None:
+                line["cpu_baseline"]["reference_dispatch"] = ref_dispatch
             line["parity"] = parity(o, st, *ref[::2], kind="bitwise-algorithm (same MDFIT-MAP v1 as the oracle)")
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def host_to_host(engine, b, opts, dev, steps: int) -> dict:
+    """The product call (engine.HostStaging, as fits.fit_packed runs it) timed
+    from pinned host buffers to pinned host buffers: with the mismatch counts
+    shipped (the product: the noise columns come from the assembly kernel) and
+    without (y, N only; the noise from the host library, ingest.noise, timed
+    separately)."""
+    import torch
+
+    from metadamage_amd import ingest
+
+    T = b.n_taxa
+    out = {}
+    for name, mm in (("mm_shipped", b.mm), ("y_N_only", None)):
+        stg = engine.HostStaging(T, device=dev, opts=opts, with_mm=mm is not None)
+        stg.run(b.y, b.N, mm, opts)  # warm
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            stg.run(b.y, b.N, mm, opts)
+        dt = (time.perf_counter() - t0) / steps
+        out[name] = {"value": round(T / dt, 1), "ms_per_call": round(dt * 1e3, 4),
+                     "h2d_bytes_per_taxon": 256 + (1440 if mm is not None else 0), "d2h_bytes_per_taxon": 256 + 360 + 4}
+    t0 = time.perf_counter()
+    ingest.noise(b.mm)
+    out["host_noise_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+    out["unit"] = "fits/s"
+    out["note"] = ("pinned host y,N (+mm) -> H2D -> fit -> D2H of the 32 record columns, predictions, status; "
+                   "stream-synchronised per call; the product ships mm (the host noise path costs more CPU than "
+                   "the PCIe it saves while the multi-file pipeline is host-bound, DESIGN.md 10)")
+    return out
 
 
 def nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, b, smp):
@@ -306,7 +386,7 @@ def nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, 
         "status_ok_frac": float((st == 0).mean()),
     }
     if not args.no_cpu_baseline and world == 1:
-        line["cpu_baseline"], ref = cpu_baseline_nuts(b, args.cpu_threads)
+        line["cpu_baseline"], ref = cpu_baseline_nuts(b, args.cpu_threads or host_cores()[0])
         line["parity"] = nuts_parity(smp, st, ref)
     return line
 
@@ -374,13 +454,13 @@ def parity(out, st, ref_out, ref_st, kind: str, rtol: float = 1e-4):
     }
 
 
-def cpu_baseline_nuts(b, threads: int):
+def cpu_baseline_nuts(b, threads: int):  # threads: the core share (host_cores)
     """The CPU oracle's sampler (oracle/mdfit_nuts.c, C + OpenMP, same
     algorithm) on the first 64 taxa of the workload."""
     from oracle.oracle import OracleLib
 
     lib = OracleLib()
-    nthr = threads if threads > 0 else min(16, os.cpu_count() or 1)
+    nthr = threads if threads > 0 else host_cores()[0]
     n = 64
     t0 = time.perf_counter()
     ref = lib.nuts_batch(b.y[:n], b.N[:n], b.mm[:n], threads=nthr, keep_samples=True)
@@ -400,29 +480,34 @@ def cpu_baseline_nuts(b, threads: int):
     }, ref
 
 
-def cpu_baseline(b, threads: int):
+def cpu_baseline(b, cores: int, visible: int):
     """The CPU oracle (oracle/libmdfit_oracle.c, C + OpenMP, same algorithm)
-    on the same workload, timed on this host's cores."""
+    on the whole workload, timed on this host's core share: median of 5."""
     from oracle.oracle import OracleLib
 
     lib = OracleLib()
-    nthr = threads if threads > 0 else min(16, os.cpu_count() or 1)
-    lib.fit_batch(b.y[:200], b.N[:200], b.mm[:200], threads=nthr)  # warm
-    t0 = time.perf_counter()
-    ref = lib.fit_batch(b.y, b.N, b.mm, threads=nthr)
-    dt = time.perf_counter() - t0
-    n1 = 500
+    lib.fit_batch(b.y[:200], b.N[:200], b.mm[:200], threads=cores)  # warm
+    times, ref = [], None
+    for _ in range(5):
+        t0 = time.perf_counter()
+        ref = lib.fit_batch(b.y, b.N, b.mm, threads=cores)
+        times.append(time.perf_counter() - t0)
+    dt = float(np.median(times))
+    n1 = 300
     t1 = time.perf_counter()
     lib.fit_batch(b.y[:n1], b.N[:n1], b.mm[:n1], threads=1)
     d1 = time.perf_counter() - t1
     return {
         "value": round(b.n_taxa / dt, 1),
         "unit": "fits/s",
-        "cores": nthr,
+        "cores": cores,
+        "host_cpus_visible": visible,
         "kind": "port",
-        "sample": f"all {b.n_taxa} taxa of the rank-0 workload on {nthr} OpenMP threads ({dt:.2f} s); "
-        f"1-thread rate on the first {n1}: {n1 / d1:.1f} fits/s",
+        "sample": f"all {b.n_taxa} taxa of the rank-0 workload on {cores} OpenMP threads, median of 5 runs "
+        f"({dt:.2f} s; min {min(times):.2f}, max {max(times):.2f}); 1-thread rate on the first {n1}: "
+        f"{n1 / d1:.1f} fits/s",
         "single_thread_value": round(n1 / d1, 1),
+        "note": "cores = the process's CPU share (affinity / OMP_NUM_THREADS: 16 per GPU on the box)",
     }, ref
 
 

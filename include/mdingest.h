@@ -89,6 +89,16 @@ int mdi_gather(int64_t rows, const int64_t* perm, int64_t n_keep, const int64_t*
                const int64_t* y_sum_total, int n_threads, uint32_t* o_nal, int8_t* o_position,
                uint32_t* o_counts16, uint32_t* o_ref2, float* o_f2, uint32_t* o_y_sum_total);
 
+/* mdi_noise: add_noise_estimates (fits.py:359-376) of n_taxa packed taxa on
+ * the host, so the 1,440 B/taxon of mismatch counts need not cross PCIe:
+ * mm = uint32[n_taxa][30][12] (columns AC AG AT CA CG CT GA GC GT TA TC TG,
+ * rows z = 1..15 then -1..-15, the layout of include/mdfit.h), out3 =
+ * double[n_taxa][3] = (normalized_noise, _forward, _reverse): per column the
+ * counts over its mean (CT forward / GA reverse excluded), then the
+ * population sd over all / forward / reverse rows (NaN when empty).
+ * n_threads <= 0: hardware concurrency. */
+int mdi_noise(const uint32_t* mm, int64_t n_taxa, int n_threads, double* out3);
+
 /* message of the last failed mdi_select / mdi_gather on this thread */
 const char* mdi_counts_error(void);
 

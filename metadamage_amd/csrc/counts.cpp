@@ -221,3 +221,77 @@ int mdi_gather(int64_t rows, const int64_t* perm, int64_t n_keep, const int64_t*
 const char* mdi_counts_error(void) { return g_cerr; }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// mdi_noise: fits.py:359-376 per packed taxon (the oracle's noise() is the check)
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int kNPos = 30, kNHalf = 15, kNMM = 12, kCT = 5, kGA = 6;
+
+void noise_one(const uint32_t* mm, double* out3) {
+  // per column: 1 / mean over its valid rows (CT forward, GA reverse excluded);
+  // a column of zeros has mean 0 -> every X = 0/0 = NaN -> dropped (np.nanstd).
+  // Branch-free over the fixed 30 x 12 block: a 0/1 weight per entry.
+  double inv[kNMM], okc[kNMM];
+  for (int j = 0; j < kNMM; ++j) {
+    uint64_t s = 0;
+    for (int i = 0; i < kNPos; ++i) {
+      const bool ex = (j == kCT && i < kNHalf) || (j == kGA && i >= kNHalf);
+      s += ex ? 0u : mm[i * kNMM + j];
+    }
+    const int cnt = (j == kCT || j == kGA) ? kNHalf : kNPos;
+    okc[j] = s != 0 ? 1.0 : 0.0;
+    inv[j] = s != 0 ? (double)cnt / (double)s : 0.0;
+  }
+  double x[kNPos][kNMM], w[kNPos][kNMM];
+  double sum[2] = {0.0, 0.0}, cnt[2] = {0.0, 0.0};
+  for (int i = 0; i < kNPos; ++i) {
+    const int h = i >= kNHalf;
+    double sh = 0.0, ch = 0.0;
+    for (int j = 0; j < kNMM; ++j) {
+      const double ex = ((j == kCT && i < kNHalf) || (j == kGA && i >= kNHalf)) ? 0.0 : 1.0;
+      w[i][j] = ex * okc[j];
+      x[i][j] = mm[i * kNMM + j] * inv[j];
+      sh += w[i][j] * x[i][j];
+      ch += w[i][j];
+    }
+    sum[h] += sh;
+    cnt[h] += ch;
+  }
+  const double mean[3] = {(sum[0] + sum[1]) / (cnt[0] + cnt[1]), sum[0] / cnt[0], sum[1] / cnt[1]};
+  double ss[3] = {0.0, 0.0, 0.0};
+  for (int i = 0; i < kNPos; ++i) {
+    const int h = i >= kNHalf;
+    const double mh = mean[1 + h];
+    double s0 = 0.0, s1 = 0.0;
+    for (int j = 0; j < kNMM; ++j) {
+      const double d0 = x[i][j] - mean[0], d1 = x[i][j] - mh;
+      s0 += w[i][j] * d0 * d0;
+      s1 += w[i][j] * d1 * d1;
+    }
+    ss[0] += s0;
+    ss[1 + h] += s1;
+  }
+  const double n3[3] = {cnt[0] + cnt[1], cnt[0], cnt[1]};
+  for (int r = 0; r < 3; ++r) out3[r] = n3[r] > 0.0 ? __builtin_sqrt(ss[r] / n3[r]) : __builtin_nan("");
+}
+}  // namespace
+
+extern "C" int mdi_noise(const uint32_t* mm, int64_t n_taxa, int n_threads, double* out3) {
+  if (n_taxa < 0 || (n_taxa > 0 && (!mm || !out3))) return MDI_E_ARG;
+  if (n_taxa == 0) return 0;
+  int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+  if (nt < 1) nt = 1;
+  if ((int64_t)nt > (n_taxa + 511) / 512) nt = (int)((n_taxa + 511) / 512);
+  std::vector<std::thread> pool;
+  const int64_t per = (n_taxa + nt - 1) / nt;
+  for (int k = 0; k < nt; ++k) {
+    const int64_t a = k * per, b = std::min(n_taxa, a + per);
+    if (a >= b) break;
+    pool.emplace_back([=] {
+      for (int64_t t = a; t < b; ++t) noise_one(mm + t * kNPos * kNMM, out3 + 3 * t);
+    });
+  }
+  for (auto& th : pool) th.join();
+  return 0;
+}

@@ -130,6 +130,75 @@ def fit_batch(y, N, mm=None, opts: _lib.MdfitOpts | None = None, device="cuda"):
     return res.out.cpu().numpy(), res.pred.cpu().numpy(), res.status.cpu().numpy()
 
 
+class HostStaging:
+    """Pinned host buffers + device tensors for host-to-host fits of up to
+    `capacity` taxa (the product call): y, N go up (256 B per taxon) and,
+    with_mm, the mismatch counts (1,440 B; without them the noise columns
+    come back NaN and ingest.noise computes them on the host); the 32 record
+    columns (25 results + 7 reserved), the predictions and the status come
+    back (652 B per taxon).  All copies are stream-ordered on `stream`."""
+
+    def __init__(self, capacity: int, device="cuda", opts: _lib.MdfitOpts | None = None, with_pred: bool = True,
+                 with_mm: bool = True):
+        torch = _torch()
+        self.capacity = int(capacity)
+        self.device = torch.device(device)
+        T = self.capacity
+        self.h_y = torch.empty((T, _lib.LD), dtype=torch.int32).pin_memory()
+        self.h_N = torch.empty((T, _lib.LD), dtype=torch.int32).pin_memory()
+        self.h_mm = torch.empty((T, _lib.NPOS, _lib.NMM), dtype=torch.int32).pin_memory() if with_mm else None
+        self.h_out = torch.empty((T, 32), dtype=torch.float64).pin_memory()
+        self.h_pred = torch.empty((T, _lib.NPRED, _lib.NPOS), dtype=torch.float32).pin_memory() if with_pred else None
+        self.h_status = torch.empty((T,), dtype=torch.int32).pin_memory()
+        self.d_y = torch.empty((T, _lib.LD), dtype=torch.int32, device=self.device)
+        self.d_N = torch.empty((T, _lib.LD), dtype=torch.int32, device=self.device)
+        self.d_mm = torch.empty((T, _lib.NPOS, _lib.NMM), dtype=torch.int32, device=self.device) if with_mm else None
+        self.res = alloc_outputs(T, device=self.device, with_pred=with_pred, opts=opts)
+
+    def run(self, y, N, mm=None, opts: _lib.MdfitOpts | None = None, stream=None, sync: bool = True):
+        """Fit the first len(y) taxa; returns numpy views (out[:, :32], pred,
+        status) of the pinned buffers (valid until the next run)."""
+        torch = _torch()
+        T = int(y.shape[0])
+        if T > self.capacity:
+            raise ValueError(f"{T} taxa > staging capacity {self.capacity}")
+        self.h_y[:T].numpy()[:] = np.asarray(y, dtype=np.uint32).view(np.int32)
+        self.h_N[:T].numpy()[:] = np.asarray(N, dtype=np.uint32).view(np.int32)
+        use_mm = mm is not None and self.h_mm is not None
+        if use_mm:
+            self.h_mm[:T].numpy()[:] = np.asarray(mm, dtype=np.uint32).view(np.int32)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(s):
+            self.d_y[:T].copy_(self.h_y[:T], non_blocking=True)
+            self.d_N[:T].copy_(self.h_N[:T], non_blocking=True)
+            if use_mm:
+                self.d_mm[:T].copy_(self.h_mm[:T], non_blocking=True)
+            res = FitBatch(self.res.out[:T], self.res.pred[:T] if self.res.pred is not None else None,
+                           self.res.status[:T], self.res.workspace)
+            fit_batch_device(self.d_y[:T], self.d_N[:T], self.d_mm[:T] if use_mm else None, opts, res, stream=s)
+            self.h_out[:T].copy_(res.out[:, :32], non_blocking=True)
+            if res.pred is not None:
+                self.h_pred[:T].copy_(res.pred, non_blocking=True)
+            self.h_status[:T].copy_(res.status, non_blocking=True)
+        if sync:
+            s.synchronize()
+        pred = self.h_pred[:T].numpy() if self.h_pred is not None else None
+        return self.h_out[:T].numpy(), pred, self.h_status[:T].numpy()
+
+
+def fit_batch_host(y, N, mm=None, opts: _lib.MdfitOpts | None = None, noise=None, device="cuda"):
+    """The product's host-to-host fit: (out[T, 32], pred, status).  mm goes
+    to the device (the assembly computes the noise columns); without it,
+    `noise` (float64[T][3], ingest.noise) fills them when given."""
+    st = HostStaging(int(np.asarray(y).shape[0]), device=device, opts=opts, with_mm=mm is not None)
+    out, pred, status = st.run(y, N, mm, opts)
+    out, pred, status = out.copy(), pred.copy(), status.copy()
+    if mm is None and noise is not None:
+        ok = status != _lib.INVALID
+        out[ok, _lib.RESULT_FIELDS.index("normalized_noise"):_lib.NRESULT] = np.asarray(noise)[ok]
+    return out, pred, status
+
+
 def special(x, device="cuda"):
     """(lgamma, digamma, trigamma) of x on the device (parity tests)."""
     torch = _torch()

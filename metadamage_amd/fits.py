@@ -173,8 +173,12 @@ def fit_packed(p: Packed, opts=None, shard: bool = True):
     world = dist.get_world_size() if shard and dist.is_available() and dist.is_initialized() else 1
     rank = dist.get_rank() if world > 1 else 0
     dev = torch.device("cuda", torch.cuda.current_device())
+    # add_noise_estimates (fits.py:359-376) runs in the assembly kernel on the
+    # shipped mismatch counts: 1,440 B/taxon of asynchronous PCIe (~0.3 ms per
+    # 10k taxa) is cheaper than the host statistics (ingest.noise: ~4 ms of CPU
+    # per 10k on 8 threads) while the multi-file pipeline is host-bound
     if world == 1:
-        return engine.fit_batch(p.y, p.N, p.mm, opts)
+        return engine.fit_batch_host(p.y, p.N, p.mm, opts)
     lo, hi = shard_range(p.n_taxa, rank, world)
     if opts is not None:  # the sampler's streams are keyed by the global taxon index
         opts = _lib.MdfitOpts.from_buffer_copy(opts)
@@ -182,7 +186,8 @@ def fit_packed(p: Packed, opts=None, shard: bool = True):
     cap = shard_capacity(p.n_taxa, world)
     rec = alloc_records(cap, dev)
     if hi > lo:
-        ty, tN, tm = engine.to_device_counts(p.y[lo:hi], p.N[lo:hi], p.mm[lo:hi], device=dev)
+        ty, tN, tm = engine.to_device_counts(p.y[lo:hi], p.N[lo:hi], p.mm[lo:hi] if p.mm is not None else None,
+                                             device=dev)
         engine.fit_batch_device(ty, tN, tm, opts, engine.FitBatch(rec.out[: hi - lo], rec.pred[: hi - lo],
                                                                    rec.status[: hi - lo]))
     buf = rec.stage()

@@ -58,8 +58,25 @@ def _load():
                                    ctypes.c_char_p, vp, ctypes.c_int, vp, vp, vp, vp, vp, vp]
         lib.mdi_gather.restype = ctypes.c_int
         lib.mdi_counts_error.restype = ctypes.c_char_p
+        lib.mdi_noise.argtypes = [vp, i64, ctypes.c_int, vp]
+        lib.mdi_noise.restype = ctypes.c_int
         _LIB = lib
     return _LIB
+
+
+def noise(mm: np.ndarray, n_threads: int = 0) -> np.ndarray:
+    """add_noise_estimates (fits.py:359-376) of packed taxa on the host
+    (mdi_noise): mm uint32[T][30][12] -> float64[T][3] (normalized_noise,
+    _forward, _reverse).  The fit then needs no mismatch counts on the GPU."""
+    mm = np.ascontiguousarray(mm, dtype=np.uint32)
+    T = mm.shape[0]
+    if mm.shape != (T, 30, 12):
+        raise ValueError(f"mm must be uint32[T][30][12], got {mm.shape}")
+    out = np.empty((T, 3))
+    rc = _load().mdi_noise(mm.ctypes.data, T, int(n_threads), out.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"mdi_noise failed ({rc})")
+    return out
 
 
 @dataclass

@@ -232,3 +232,24 @@ def test_native_pipeline_uint32_overflow(tmp_path):
     g.write_text(row(1, 100, 0, 5) + row(2, 3, 0, 2**32))  # taxon 2 fails min_alignments
     df = ingest.compute_counts(_cfg(g))
     assert list(df["tax_id"].astype(int).unique()) == [1]
+
+
+def test_native_noise_matches_the_reference_restatement():
+    """ingest.noise (mdi_noise, the host form of add_noise_estimates,
+    fits.py:359-376) against the numpy restatement pinned to the reference's
+    own add_noise_estimates (oracle.noise): zero columns, an all-zero taxon,
+    a zero half."""
+    from metadamage_amd import ingest
+    from metadamage_amd.synthetic import generate
+    from oracle import oracle as orc
+
+    b = generate(300, seed=8)
+    b.mm[5] = 0
+    b.mm[6, :, 3] = 0
+    b.mm[7, :15, :] = 0
+    b.mm[8, :, 5] = 0
+    nz = ingest.noise(b.mm)
+    ref = np.array([orc.noise(b.mm[i]) for i in range(b.n_taxa)])
+    assert np.array_equal(np.isnan(nz), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    assert (np.abs(nz[ok] - ref[ok]) <= 1e-13 * np.abs(ref[ok])).all()

@@ -115,28 +115,33 @@ def fit_taxon(args):
     return n_sigma, asym
 
 
+def measure(taxa: int = 1000, cores: int = 16) -> dict:
+    """The reference-dispatch-shape rate on the first `taxa` taxa of C2."""
+    from metadamage_amd.synthetic import generate
+
+    b = generate(max(taxa, 1), seed=1)  # C2's workload (seed 1); its first taxa
+    tasks = [(b.y[i, :30], b.N[i, :30]) for i in range(taxa)]
+    t0 = time.perf_counter()
+    out = []
+    for lo in range(0, taxa, 1000):  # a new Pool per 1,000-taxon chunk, as fits.py:692-706
+        with Pool(cores) as pool:
+            out += pool.map(fit_taxon, tasks[lo:lo + 1000])
+    dt = time.perf_counter() - t0
+    return {
+        "kind": "python-restatement in the reference's dispatch shape (Pool per 1,000-taxon chunk, scipy "
+                "L-BFGS-B MAP per sub-fit); numpyro itself is not installed",
+        "value": round(taxa / dt, 2), "unit": "fits/s", "cores": cores,
+        "sample": f"the first {taxa} taxa of C2 (seed 1), {dt:.2f} s including Pool start-up; extrapolated rate",
+        "finite_n_sigma": float(np.isfinite([o[0] for o in out]).mean()),
+    }
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--taxa", type=int, default=1000)
     ap.add_argument("--cores", type=int, default=min(16, os.cpu_count() or 1))
     a = ap.parse_args()
-    from metadamage_amd.synthetic import generate
-
-    b = generate(10_000, seed=1)  # C2's workload; the first --taxa taxa
-    tasks = [(b.y[i, :30], b.N[i, :30]) for i in range(a.taxa)]
-    t0 = time.perf_counter()
-    out = []
-    for lo in range(0, a.taxa, 1000):  # a new Pool per 1,000-taxon chunk, as fits.py:692-706
-        with Pool(a.cores) as pool:
-            out += pool.map(fit_taxon, tasks[lo:lo + 1000])
-    dt = time.perf_counter() - t0
-    print(json.dumps({
-        "kind": "python-restatement in the reference's dispatch shape (Pool per 1,000-taxon chunk, scipy "
-                "L-BFGS-B MAP per sub-fit); numpyro itself is not installed",
-        "value": round(a.taxa / dt, 2), "unit": "fits/s", "cores": a.cores,
-        "sample": f"the first {a.taxa} taxa of C2 (seed 1), {dt:.2f} s including Pool start-up; extrapolated rate",
-        "finite_n_sigma": float(np.isfinite([o[0] for o in out]).mean()),
-    }), flush=True)
+    print(json.dumps(measure(a.taxa, a.cores)), flush=True)
 
 
 if __name__ == "__main__":
