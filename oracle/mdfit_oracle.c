@@ -609,6 +609,11 @@ static void noise(const uint32_t* mm, double out3[3]) {
  * BetaBinomial(D phi, (1-D) phi, N) (MDFIT-HPDI v1, mdfit_hpdi.c); NaN when
  * N = 0 (the reference divides 0 draws by N = 0, fits.py:115).  want_hpdi = 0:
  * the median only (D_max_forward / _reverse). */
+/* tests may switch the HPDI off (oracle_set_hpdi(0)) to check the other
+ * columns of a large batch quickly; the HPDI columns are then NaN */
+static int g_hpdi_on = 1;
+void oracle_set_hpdi(int on) { g_hpdi_on = on != 0; }
+
 static void predict(double A, double q, double c, double phi, int k, double N,
                     double o[3], int want_hpdi) {
   if (N == 0) {
@@ -619,7 +624,7 @@ static void predict(double A, double q, double c, double phi, int k, double N,
   if (D > 1.0) D = 1.0;
   o[0] = D;
   o[1] = o[2] = NAN;
-  if (want_hpdi) {
+  if (want_hpdi && g_hpdi_on) {
     double lo, hi;
     hp_window(N, D * phi, (1.0 - D) * phi, &lo, &hi);
     o[1] = lo / N;

@@ -1,0 +1,149 @@
+"""GPU tests at the BASELINE.json configurations beyond the C2 bench size:
+
+  * C4's per-GPU share (1M TaxIDs / 8 = 125k, seed 3): every taxon against the
+    CPU oracle (all result columns; the predictive HPDI on a sample -- the
+    oracle's long-double HPDI is the slow part of the checker);
+  * C3 (100k TaxIDs, the reference's NUTS, seed 2): status and finiteness of
+    every record, sampler streams keyed by the global taxon index (a slice
+    refitted on its own with index_base reproduces the full run's records),
+    and posterior means vs the oracle's chains on a 64-taxon subsample;
+  * C5 (the streamed counts -> fits pipeline, main.main over several files):
+    2 synthetic 22-column files x 20k TaxIDs with 5 % built to fail the cuts,
+    the parquet outputs against the oracle fit of the packed counts.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from tests.helpers import RTOL, mixed_rel
+
+pytestmark = pytest.mark.gpu
+
+HPDI_COLS = (2, 3)  # D_max_lower_hpdi, D_max_upper_hpdi
+
+
+@pytest.fixture(scope="module")
+def engine():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test selected but no HIP device is visible")
+    from metadamage_amd import engine as eng
+
+    return eng
+
+
+def test_c4_per_gpu_share_vs_oracle(engine, oracle_lib):
+    from metadamage_amd.synthetic import generate
+
+    b = generate(125_000, seed=3)
+    out, pred, st = engine.fit_batch(b.y, b.N, b.mm)
+    ref_out, ref_pred, ref_st = oracle_lib.fit_batch(b.y, b.N, b.mm, hpdi=False)
+    assert (st == ref_st).mean() > 0.99999, np.where(st != ref_st)[0][:10]
+    both = (st == 0) & (ref_st == 0)
+    assert both.mean() > 0.9999
+    cols = [j for j in range(25) if j not in HPDI_COLS]
+    rel = mixed_rel(out[both][:, cols], ref_out[both][:, cols])
+    assert rel.max() < RTOL, (rel.max(), np.unravel_index(rel.argmax(), rel.shape))
+    assert np.nanmax(mixed_rel(pred[both, 0], ref_pred[both, 0])) < 1e-5
+    # the predictive HPDI (D_max columns and every prediction bound) on a sample
+    idx = np.sort(np.random.default_rng(4).choice(b.n_taxa, 2000, replace=False))
+    s_out, s_pred, s_st = oracle_lib.fit_batch(b.y[idx], b.N[idx], b.mm[idx])
+    ok = (s_st == 0) & (st[idx] == 0)
+    assert mixed_rel(out[idx][ok][:, list(HPDI_COLS)], s_out[ok][:, list(HPDI_COLS)]).max() < RTOL
+    assert np.nanmax(mixed_rel(pred[idx][ok][:, 1:], s_pred[ok][:, 1:])) < RTOL
+
+
+def test_c3_nuts_100k(engine, oracle_lib):
+    import torch
+
+    from metadamage_amd import _lib
+    from metadamage_amd.synthetic import generate
+
+    T = 100_000
+    b = generate(T, seed=2)
+    opts = _lib.default_opts(mode=_lib.MODE_NUTS)
+    ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm)
+    res = engine.fit_batch_device(ty, tN, tm, opts)
+    torch.cuda.synchronize()
+    out, st = res.out.cpu().numpy(), res.status.cpu().numpy()
+    assert (st == 0).mean() > 0.999
+    assert np.isfinite(out[st == 0][:, [0, 1, 4, 5, 6, 15, 18, 21]]).all()
+    sub = 30_000 + np.arange(64)  # a contiguous subsample (one oracle call, index_base keyed)
+    smp = engine.samples_view(res, T, opts)[torch.as_tensor(sub, device=res.out.device)].cpu().numpy()
+    del res
+    # streams keyed by the global taxon index: a slice refitted alone with its
+    # index_base reproduces the full run's records bit for bit
+    lo, hi = 40_000, 41_000
+    o2 = _lib.default_opts(mode=_lib.MODE_NUTS, index_base=lo)
+    r2 = engine.fit_batch_device(ty[lo:hi].contiguous(), tN[lo:hi].contiguous(), tm[lo:hi].contiguous(), o2)
+    torch.cuda.synchronize()
+    assert np.array_equal(r2.out.cpu().numpy()[:, :25], out[lo:hi, :25], equal_nan=True)
+    assert np.array_equal(r2.status.cpu().numpy(), st[lo:hi])
+    del r2
+    # posterior means vs the oracle's chains (same sampler, same Philox streams;
+    # agreement in distribution): |mean diff| / batch-means MCSE
+    ref_out, _, ref_st, ref_smp = oracle_lib.nuts_batch(b.y[sub], b.N[sub], b.mm[sub], index_base=int(sub[0]),
+                                                        keep_samples=True)
+    assert (ref_st == st[sub]).mean() >= 0.95
+    zs = []
+    for s in range(6):
+        for j in ((0, 1, 2, 3) if s in (0, 2, 3) else (0, 3)):
+            a, r = smp[:, s, :, j], ref_smp[:, s, :, j]
+            se = np.hypot(_mcse(a), _mcse(r))
+            zs.append(np.abs(a.mean(1) - r.mean(1)) / np.maximum(se, 1e-300))
+    z = np.concatenate(zs)
+    assert np.median(z) < 1.2 and (z > 5).mean() < 0.03, (np.median(z), (z > 5).mean())
+
+
+def _mcse(x, nb=20):
+    m = x.shape[-1] // nb
+    bm = x[..., : m * nb].reshape(x.shape[:-1] + (nb, m)).mean(-1)
+    return bm.std(-1, ddof=1) / np.sqrt(nb)
+
+
+def test_c5_streamed_files(tmp_path, oracle_lib):
+    from metadamage_amd import _lib, fits, io, main, utils
+    from metadamage_amd.synthetic import generate, to_counts_table
+
+    files = []
+    for i in range(2):
+        f = tmp_path / f"c5_{i}.txt"
+        to_counts_table(generate(20_000, seed=100 + i, fail_fraction=0.05)).to_csv(f, sep="\t", header=False,
+                                                                                   index=False)
+        files.append(f)
+    cfg = utils.Config(out_dir=tmp_path / "out", max_fits=None, max_cores=1, min_alignments=10, min_y_sum=10,
+                       substitution_bases_forward="CT", substitution_bases_reverse="GA", forced=True,
+                       version="0.0.0", inference="map")
+    results = main.main([str(f) for f in files], cfg)
+    assert len(results) == 2
+    for f in files:
+        c = utils.Config(out_dir=tmp_path / "out", max_fits=None, max_cores=1, min_alignments=10, min_y_sum=10,
+                         substitution_bases_forward="CT", substitution_bases_reverse="GA", forced=True,
+                         version="0.0.0", inference="map")
+        c.add_filename(str(f))
+        dfr, dfp = results[c.shortname]
+        # the parquet files hold the frames the driver returned
+        assert io.Parquet(c.filename_fit_results).load().equals(dfr)
+        assert len(io.Parquet(c.filename_fit_predictions).load()) == len(dfp) == 30 * len(dfr)
+        # the packed counts the driver fitted, fitted again by the oracle
+        df_counts = io.Parquet(c.filename_counts).load()
+        p = fits.pack_counts(df_counts, c)
+        assert 0.9 * 20_000 < p.n_taxa < 20_000  # ~5 % fail the cuts
+        ref_out, _, ref_st = oracle_lib.fit_batch(p.y, p.N, p.mm, hpdi=False)
+        keep = ref_st == _lib.OK
+        assert len(dfr) >= keep.sum() - 2  # the GPU keeps (status 0) what the oracle keeps, +- rounding
+        got = dfr.set_index(dfr["tax_id"].astype(np.int64))
+        tids = np.asarray(p.tax_id, dtype=np.int64)[keep]
+        common = np.intersect1d(tids, got.index.to_numpy())
+        assert common.size >= keep.sum() - 2
+        rows = {t: i for i, t in enumerate(np.asarray(p.tax_id, dtype=np.int64))}
+        ri = np.array([rows[t] for t in common])
+        for j, name in enumerate(_lib.RESULT_FIELDS):
+            if j in HPDI_COLS:
+                continue
+            a = got.loc[common, name].to_numpy(np.float64)
+            r = ref_out[ri, j].astype(np.float32).astype(np.float64)  # the frames store float32
+            assert mixed_rel(a, r).max() < RTOL, (f.name, name, mixed_rel(a, r).max())

@@ -1,0 +1,80 @@
+"""GPU test of the product's multi-GPU branch (fits.fit_packed with
+world > 1): two ranks under the gloo backend share cuda:0,
+each fits its contiguous taxon shard with the HIP kernels, the packed records
+are staged to the host and gathered once to rank 0 -- and the gathered
+records must equal the single-process fit bit for bit (the fit of a taxon
+does not depend on its batch: tests/test_gpu_parity.py's order-independence;
+the sampler's streams are keyed by the global taxon index)."""
+
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank(rank, world, port, T, mode, q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)  # both ranks on the one GPU of the box
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from metadamage_amd import _lib, fits
+        from metadamage_amd.synthetic import generate
+
+        b = generate(T, seed=23)
+        p = fits.Packed(b.tax_id, b.tax_id.astype(str), np.full(T, "species"), b.N_alignments, b.y, b.N, b.mm)
+        opts = _lib.default_opts(mode=mode, num_warmup=20, num_samples=40) if mode == _lib.MODE_NUTS else None
+        res = fits.fit_packed(p, opts, shard=True)
+        q.put((rank, None if res is None else [np.asarray(a) for a in res]))
+    except Exception as e:  # surfaced by the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode_name", ["map", "nuts"])
+def test_sharded_fit_packed_equals_single_process(mode_name):
+    import torch
+    import torch.multiprocessing as mp
+
+    from metadamage_amd import _lib, fits
+    from metadamage_amd.synthetic import generate
+
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test selected but no HIP device is visible")
+    mode = _lib.MODE_NUTS if mode_name == "nuts" else _lib.MODE_MAP
+    T = 1501 if mode == _lib.MODE_MAP else 61  # ragged shards
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, T, mode, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    got = dict(q.get(timeout=600) for _ in procs)
+    for pr in procs:
+        pr.join(timeout=120)
+    assert got[1] is None, got[1]
+    assert not isinstance(got[0], str), got[0]
+    out, pred, st = got[0]
+    # the single-process reference: the same packed taxa, one call
+    b = generate(T, seed=23)
+    p = fits.Packed(b.tax_id, b.tax_id.astype(str), np.full(T, "species"), b.N_alignments, b.y, b.N, b.mm)
+    opts = _lib.default_opts(mode=mode, num_warmup=20, num_samples=40) if mode == _lib.MODE_NUTS else None
+    ref_out, ref_pred, ref_st = fits.fit_packed(p, opts, shard=False)
+    assert out.shape == (T, 32) and ref_out.shape == (T, 32)
+    assert np.array_equal(st, ref_st)
+    assert np.array_equal(out[:, :_lib.NRESULT], ref_out[:, :_lib.NRESULT], equal_nan=True)
+    assert np.array_equal(pred, ref_pred, equal_nan=True)
