@@ -217,6 +217,8 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
   int running = 0;
   double u[4] = {0, 0, 0, 0}, ut[4] = {0, 0, 0, 0}, d[4] = {0, 0, 0, 0};
   double curF = INFINITY, curMag = 0.0, curPg = 0.0, t = 1.0;
+  double curG3 = 0.0, curGd = 0.0;  // g_3 and g.d at the current point (exhaustion rules)
+  bool rescued = false, relax = false;  // the flat-tail rescue (oracle: fit_one), once per fit
   int evals = 0, status = MDFIT_MAXITER;
   int first = 1;
 #ifdef MDFIT_STAMP
@@ -308,6 +310,7 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       for (int j = 0; j < 4; ++j) ut[j] = u[j];
       curF = INFINITY;
       curMag = curPg = 0.0;
+      rescued = relax = false;
       t = 1.0;
       evals = 0;
       status = MDFIT_MAXITER;
@@ -381,8 +384,9 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         }
       } else {
         accept = isfinite(tr.F) &&
-                 (tr.F < curF || (tr.F <= curF + kNoiseF * (curMag + fabs(curF)) && pgt < curPg));
+                 (tr.F < curF || (tr.F <= curF + kNoiseF * (curMag + fabs(curF)) && (relax || pgt < curPg)));
       }
+      relax = false;
       if (accept) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) u[j] = ut[j];
@@ -391,6 +395,8 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         curPg = pgt;
         if (!done) {
           newton_dir(pa.pmd, u, tr.g, tr.H, pgt, d);
+          curG3 = tr.g[3];
+          curGd = tr.g[0] * d[0] + tr.g[1] * d[1] + tr.g[2] * d[2] + tr.g[3] * d[3];
           t = 1.0;
           if (maxabs4(d) <= tol) {
             done = true;
@@ -399,9 +405,21 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         }
       } else {
         t *= 0.5;
-        if (t < 1e-12) {
-          done = true;
-          status = (maxabs4(d) <= 1e-5 || curPg <= kPgTol) ? MDFIT_OK : MDFIT_MAXITER;
+        if (t < 1e-12) {  // line search exhausted (oracle: fit_one)
+          if (!rescued && u[3] < 0.0 && d[3] < 0.0 && u[3] > kULo[3]) {
+            // the flat tail of log delta: jump onto its lower bound once
+            rescued = relax = true;
+            d[0] = d[1] = d[2] = 0.0;
+            d[3] = kULo[3] - u[3];
+            curGd = curG3 * d[3];
+            t = 1.0;
+          } else {
+            done = true;
+            status = (maxabs4(d) <= 1e-5 || curPg <= kPgTol ||
+                      fabs(curGd) <= kNoiseF * (curMag + fabs(curF)))
+                         ? MDFIT_OK
+                         : MDFIT_MAXITER;
+          }
         }
       }
       if (!done && evals >= max_iter) {

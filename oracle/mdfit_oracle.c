@@ -428,14 +428,16 @@ static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
     status = MDFIT_OK;
     goto done;
   }
+  int rescued = 0, relax = 0; /* the flat-tail rescue (below): once per fit */
   while (evals < max_iter) {
     for (int j = 0; j < 4; j++) ut[j] = clampd(u[j] + t * d[j], U_LO[j], U_HI[j]);
     evaluate(model, y, N, lo, hi, ut, &tr);
     evals++;
+    const double noise = NOISE_F * (cur.mag + fabs(cur.F));
     int acc = isfinite(tr.F) &&
               (tr.F < cur.F ||
-               (tr.F <= cur.F + NOISE_F * (cur.mag + fabs(cur.F)) &&
-                pgnorm(ut, tr.g) < pgnorm(u, cur.g)));
+               (tr.F <= cur.F + noise && (relax || pgnorm(ut, tr.g) < pgnorm(u, cur.g))));
+    relax = 0;
     if (g_trace)
       printf("%d trF=%.12f curF=%.12f acc=%d t=%.3g |d|=%.3e |gt|=%.3e |gc|=%.3e u=[%.10f %.10f %.10f %.10f] d=[%.3e %.3e %.3e %.3e]\n",
              evals, tr.F, cur.F, acc, t, maxabs4(d), maxabs4(tr.g), maxabs4(cur.g), u[0], u[1], u[2], u[3], d[0], d[1], d[2], d[3]);
@@ -450,10 +452,23 @@ static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
       }
     } else {
       t *= 0.5;
-      if (t < 1e-12) { /* line search exhausted: numerically at the optimum when
-                          * the step or the projected gradient is negligible (the
-                          * latter: phi creeping to its bound along a flat exp tail) */
-        status = (maxabs4(d) <= 1e-5 || pgnorm(u, cur.g) <= PG_TOL) ? MDFIT_OK : MDFIT_MAXITER;
+      if (t < 1e-12) { /* line search exhausted */
+        /* the flat tail of log delta (phi -> 2): the Newton step heads down a
+         * tail in which F changes below its rounding scale, so the stopping
+         * point would depend on the rounding path.  Once per fit: jump log delta
+         * onto its lower bound (the limit of that walk; accepted within F's
+         * rounding scale) and continue from there. */
+        if (!rescued && u[P_D] < 0.0 && d[P_D] < 0.0 && u[P_D] > U_LO[P_D]) {
+          rescued = relax = 1;
+          for (int j = 0; j < 4; j++) d[j] = j == P_D ? U_LO[P_D] - u[P_D] : 0.0;
+          t = 1.0;
+          continue;
+        }
+        /* numerically at the optimum when the step, the projected gradient or
+         * the step's predicted decrease |g.d| is below F's resolution */
+        double gd = 0;
+        for (int j = 0; j < 4; j++) gd += cur.g[j] * d[j];
+        status = (maxabs4(d) <= 1e-5 || pgnorm(u, cur.g) <= PG_TOL || fabs(gd) <= noise) ? MDFIT_OK : MDFIT_MAXITER;
         break;
       }
     }

