@@ -155,6 +155,13 @@ constexpr int kPrioEvals = 15;  // fit length (evaluations) that raises the wave
 // started at the all-position mode (still in registers; the counts too --
 // PPL 2 re-deals them to the pair layout with lane shuffles), so a pair costs
 // no memory round trip and no hand-off between waves.
+// line-search state bits (fit_kernel): the saddle escape's H indefinite at the
+// current point, re-evaluation pending, escape line search running,
+// exhaustion status OK, the escape count (kEscCount, in units of kEscN: at
+// most 4); the flat-tail rescue done / its relaxed acceptance pending
+constexpr unsigned kEscIndef = 1u, kEscProbe = 2u, kEscNc = 4u, kEscExhOk = 8u, kEscN = 16u, kEscCount = 0x70u,
+                   kEscRescued = 0x100u, kEscRelax = 0x200u;
+
 template <int PPL>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_FIT_WAVES_PER_EU)))
 void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN, int64_t T,
@@ -218,7 +225,9 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
   double u[4] = {0, 0, 0, 0}, ut[4] = {0, 0, 0, 0}, d[4] = {0, 0, 0, 0};
   double curF = INFINITY, curMag = 0.0, curPg = 0.0, t = 1.0;
   double curG3 = 0.0, curGd = 0.0;  // g_3 and g.d at the current point (exhaustion rules)
-  bool rescued = false, relax = false;  // the flat-tail rescue (oracle: fit_one), once per fit
+  // the flat-tail rescue and the saddle escape (oracle: fit_one) in one word:
+  // kEsc* flags + escapes x kEscN (per-lane bools would cost SGPR-pair masks)
+  unsigned esc = 0u;
   int evals = 0, status = MDFIT_MAXITER;
   int first = 1;
 #ifdef MDFIT_STAMP
@@ -310,7 +319,7 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       for (int j = 0; j < 4; ++j) ut[j] = u[j];
       curF = INFINITY;
       curMag = curPg = 0.0;
-      rescued = relax = false;
+      esc = 0u;
       t = 1.0;
       evals = 0;
       status = MDFIT_MAXITER;
@@ -374,8 +383,14 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       finish_eval(pa.pmd, th, acc, tr);
       ++evals;
       const double pgt = pgnorm(ut, tr.g);  // projected gradient at the trial point
-      bool accept, done = false;
-      if (first) {
+      bool accept = false, done = false;
+      // the saddle escape's re-evaluation at u (same F, g, H as the current
+      // point) goes through the acceptance below; its H gives the direction
+      const bool probed = esc & kEscProbe;
+      esc &= ~kEscProbe;
+      if (probed) {
+        accept = true;
+      } else if (first) {
         accept = true;
         first = false;
         if (!isfinite(tr.F)) {
@@ -383,42 +398,67 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
           status = MDFIT_NONFINITE;
         }
       } else {
+        const double noise = kNoiseF * (curMag + fabs(curF));
         accept = isfinite(tr.F) &&
-                 (tr.F < curF || (tr.F <= curF + kNoiseF * (curMag + fabs(curF)) && (relax || pgt < curPg)));
+                 ((esc & kEscNc) ? tr.F < curF - noise : (tr.F < curF || (tr.F <= curF + noise && ((esc & kEscRelax) || pgt < curPg))));
       }
-      relax = false;
+      esc &= ~kEscRelax;
       if (accept) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) u[j] = ut[j];
         curF = tr.F;
         curMag = tr.mag;
         curPg = pgt;
+        esc &= ~kEscNc;
         if (!done) {
-          newton_dir(pa.pmd, u, tr.g, tr.H, pgt, d);
+          const bool ind = newton_dir(pa.pmd, u, tr.g, tr.H, pgt, d, probed);
           curG3 = tr.g[3];
           curGd = tr.g[0] * d[0] + tr.g[1] * d[1] + tr.g[2] * d[2] + tr.g[3] * d[3];
           t = 1.0;
-          if (maxabs4(d) <= tol) {
-            done = true;
-            status = MDFIT_OK;
+          if (probed) {
+            if (ind) {
+              esc += kEscN | kEscNc;
+            } else {
+              done = true;
+              status = (esc & kEscExhOk) ? MDFIT_OK : MDFIT_MAXITER;
+            }
+          } else {
+            esc = ind ? esc | kEscIndef : esc & ~kEscIndef;
+            if (maxabs4(d) <= tol) {
+              done = true;
+              status = MDFIT_OK;
+            }
           }
+        }
+      } else if (esc & kEscNc) {  // the escape finds no decrease beyond F's rounding
+        t *= 0.5;
+        if (t < 1e-3) {
+          done = true;
+          status = (esc & kEscExhOk) ? MDFIT_OK : MDFIT_MAXITER;
         }
       } else {
         t *= 0.5;
         if (t < 1e-12) {  // line search exhausted (oracle: fit_one)
-          if (!rescued && u[3] < 0.0 && d[3] < 0.0 && u[3] > kULo[3]) {
+          if (!(esc & kEscRescued) && u[3] < 0.0 && d[3] < 0.0 && u[3] > kULo[3]) {
             // the flat tail of log delta: jump onto its lower bound once
-            rescued = relax = true;
+            esc |= kEscRescued | kEscRelax;
             d[0] = d[1] = d[2] = 0.0;
             d[3] = kULo[3] - u[3];
             curGd = curG3 * d[3];
             t = 1.0;
           } else {
-            done = true;
-            status = (maxabs4(d) <= 1e-5 || curPg <= kPgTol ||
-                      fabs(curGd) <= kNoiseF * (curMag + fabs(curF)))
-                         ? MDFIT_OK
-                         : MDFIT_MAXITER;
+            const bool exh_ok =
+                maxabs4(d) <= 1e-5 || curPg <= kPgTol || fabs(curGd) <= kNoiseF * (curMag + fabs(curF));
+            esc = exh_ok ? esc | kEscExhOk : esc & ~kEscExhOk;
+            if ((esc & kEscIndef) && (esc & kEscCount) < 4u * kEscN && evals < max_iter) {
+              // the saddle escape (oracle: fit_one): re-evaluate at u next trip
+              esc |= kEscProbe;
+              d[0] = d[1] = d[2] = d[3] = 0.0;
+              t = 1.0;
+            } else {
+              done = true;
+              status = exh_ok ? MDFIT_OK : MDFIT_MAXITER;
+            }
           }
         }
       }
@@ -749,6 +789,7 @@ __global__ __launch_bounds__(kWave) void hpdi_wide_kernel(HpdiIO io, const int* 
   const int n_wide = ctr[0];  // written by K4a (stream-ordered)
   for (int64_t i = (int64_t)blockIdx.x * kWave + threadIdx.x; i < n_wide; i += (int64_t)gridDim.x * kWave) {
     const hpdi::WideRec r = recs[i];
+    HPDI_CNT(8);
     double lo, hi;
     hpdi::wide_window(r, lo, hi);
     hpdi_write<kFit>(io, r.item, r.N, lo, hi);
@@ -1072,6 +1113,15 @@ int mdfit_betabinom_logpmf(const double* y, const double* N, const double* alpha
                      (hipStream_t)hip_stream, y, N, alpha, beta, n, out, grad);
   return check_launch("betabinom_kernel");
 }
+
+#ifdef MDFIT_HPDI_COUNT
+// diagnostic: read (and zero) the HPDI loop counters
+int mdfit_hpdi_counts(unsigned long long* out32) {
+  if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(mdfit::hpdi::g_hpdi_cnt), 256) != hipSuccess) return 1;
+  const unsigned long long z[32] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(mdfit::hpdi::g_hpdi_cnt), z, 256) != hipSuccess;
+}
+#endif
 
 int mdfit_hpdi68(const double* N, const double* alpha, const double* beta, int64_t n, double* lo,
                  double* hi, void* hip_stream) {

@@ -40,13 +40,30 @@ namespace hpdi {
 #define MDFIT_HPDI_UNROLL 1
 #endif
 
+// diagnostic builds only (-DMDFIT_HPDI_COUNT): per site k, lane executions
+// [2k] and wave issues [2k+1] -- the SIMD efficiency of the loops
+#ifdef MDFIT_HPDI_COUNT
+__device__ unsigned long long g_hpdi_cnt[32];
+#define HPDI_CNT(k)                                                                  \
+  do {                                                                               \
+    atomicAdd(&::mdfit::hpdi::g_hpdi_cnt[2 * (k)], 1ull);                                         \
+    if ((int)__lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1)            \
+      atomicAdd(&::mdfit::hpdi::g_hpdi_cnt[2 * (k) + 1], 1ull);                                   \
+  } while (0)
+#else
+#define HPDI_CNT(k) ((void)0)
+#endif
+
 constexpr double kMass = 0.68;
 constexpr double kSigGreedy = 100.0;
 constexpr double kT0 = -0.49447329849;  // -Z68^2 / 2
 constexpr double kK0 = 16.0;
 constexpr double kLV = 4.0;
 constexpr double kLX = 2.5;
-constexpr double kStop = 4.0;
+#ifndef MDFIT_HPDI_STOP
+#define MDFIT_HPDI_STOP 16.0
+#endif
+constexpr double kStop = MDFIT_HPDI_STOP;  // counts: the exact fix-up walk finishes
 constexpr double kGLX[3] = {0.2386191860831969, 0.6612093864662645, 0.9324695142031521};
 constexpr double kGLW[3] = {0.4679139345726910, 0.3607615730481386, 0.1713244923791704};
 
@@ -242,6 +259,7 @@ __device__ __forceinline__ void load_pmf(Pmf& P, const WideRec& r) {
 __device__ __forceinline__ double walk_sum(const Pmf& P, double A, double B, double gA) {
   double v = fexp(gA), s = 0.0;
   for (double y = A; y <= B; y += 1.0) {
+    HPDI_CNT(6);
     s += v;
     if (y < B) v *= ratio(P, y);
   }
@@ -268,6 +286,7 @@ __device__ __forceinline__ double wide_mass(const Pmf& P, double A, double B, do
       we = B1;
     }
     if (we >= ws) {
+      HPDI_CNT(10);
       tot += walk_sum(P, ws, we, g_of(P, ws));
       if (w == 0) A1 = we + 1.0;
       else if (w == 1) B1 = ws - 1.0;
@@ -314,6 +333,7 @@ __device__ __forceinline__ double wide_mass(const Pmf& P, double A, double B, do
       for (int i = 0; i < 6; ++i) {  // independent evaluations (ILP vs registers: MDFIT_HPDI_UNROLL)
         const double gx = i < 3 ? -kGLX[2 - i] : kGLX[i - 3];
         const double gw = kGLW[i < 3 ? 2 - i : i - 3];
+        HPDI_CNT(2);
         const double v = cc + h * gx;
         const double ev = lg ? fexp(v) : 1.0;
         const double x = lg ? (snl ? ev - P.a : N + P.b - ev) : v;
@@ -327,6 +347,7 @@ __device__ __forceinline__ double wide_mass(const Pmf& P, double A, double B, do
 #pragma unroll 1
   for (int e = 0; e < 2; ++e) {
     double sx;
+    HPDI_CNT(3);
     const double gx = gfun<true>(P, e == 0 ? A1 : B1, sx);
     fe[e] = fexp(gx);
     se[e] = sx;
@@ -341,6 +362,7 @@ __device__ __forceinline__ void wide_fixup(const Pmf& P, double A, double B, dou
   double pl = A > 0.0 ? pA * rcp(ratio(P, A - 1.0)) : 0.0;
   double pr = B < N ? pB * ratio(P, B) : 0.0;
   for (int guard = 0; guard < (1 << 26); ++guard) {
+    HPDI_CNT(7);
     if (M < kMass && (pl > 0.0 || pr > 0.0)) {  // grow
       if (pl >= pr) {
         A -= 1.0;
@@ -393,11 +415,15 @@ __device__ __forceinline__ void wide_window(const WideRec& r, double& lo, double
   Pmf P;
   load_pmf(P, r);
   const double N = P.N, m = P.m, sd = r.sd, mu = r.mu;
+  // g(0), g(N) (one site) only when that end is within 4 tau of the mode
+  const double tau = sqrt(sd * sd + (mu - m) * (mu - m));
   double gE[2];
 #pragma unroll 1
-  for (int e = 0; e < 2; ++e) {  // g(0), g(N): one site
-    const bool need = e == 0 ? m > 0.0 : m < N;
-    gE[e] = need ? g_of(P, e == 0 ? 0.0 : N) : 0.0;
+  for (int e = 0; e < 2; ++e) {
+    const bool inside = e == 0 ? m > 0.0 : m < N;
+    const bool near = (e == 0 ? m : N - m) <= 4.0 * tau;
+    if (inside && near) HPDI_CNT(0);
+    gE[e] = inside ? (near ? g_of(P, e == 0 ? 0.0 : N) : -INFINITY) : 0.0;
   }
   const double g0 = gE[0], gN = gE[1];
   double t = kT0;
@@ -409,6 +435,7 @@ __device__ __forceinline__ void wide_window(const WideRec& r, double& lo, double
   double xe[2] = {m - sd, m + sd};  // two-sided ends
   double A = m, B = m, M = P.pm;
   for (int it = 0;; ++it) {
+    HPDI_CNT(9);
     bool cl = false, cr = false;
     if (one < 0) {
       cl = m == 0.0 || g0 >= t;
@@ -426,6 +453,7 @@ __device__ __forceinline__ void wide_window(const WideRec& r, double& lo, double
         double xr = fmin(fmax(xe[e], rlo), rhi);
         for (int k = 0; k < 60; ++k) {
           double sx;
+          HPDI_CNT(1);
           const double gx = gfun<true>(P, xr, sx) - t;
           if (fabs(gx) < 1e-12) break;
           if ((gx < 0.0) == rising) rlo = xr;
@@ -452,6 +480,7 @@ __device__ __forceinline__ void wide_window(const WideRec& r, double& lo, double
       const bool need = one >= 0 ? e == 0 : (e == 0 ? !cl : !cr);
       if (!need) continue;
       double sx;
+      HPDI_CNT(4);
       const double gx = gfun<true>(P, one >= 0 ? x : xe[e], sx);
       pe[e] = one >= 0 ? fexp(gx) * P.pm : sx;
     }
@@ -471,7 +500,7 @@ __device__ __forceinline__ void wide_window(const WideRec& r, double& lo, double
         xn = N + P.b - exp(log(N - x + P.b) - F / dF);
       }
       if (!(lb < xn && xn < hb)) xn = 0.5 * (lb + hb);
-      if (fabs(xn - x) < fmax(kStop, 2e-5 * x) || it >= 40) break;
+      if (fabs(xn - x) < kStop || it >= 40) break;
       x = xn;
     } else {
       if (M >= kMass) tL = t;
@@ -490,7 +519,7 @@ __device__ __forceinline__ void wide_window(const WideRec& r, double& lo, double
       double tn;
       if (Dp > 0.0) {
         const double dt = (log(M) - log(kMass)) * M / Dp;
-        if (fabs(dt) * mv < fmax(kStop, 2e-5 * A)) break;
+        if (fabs(dt) * mv < kStop) break;
         tn = t + dt;
       } else {
         tn = 0.5 * (tL + tH);  // both ends clamped: raise the level
@@ -504,6 +533,7 @@ __device__ __forceinline__ void wide_window(const WideRec& r, double& lo, double
 #pragma unroll 1
   for (int e = 0; e < 2; ++e) {
     const bool need = e == 0 || B != A;
+    if (need) HPDI_CNT(5);
     pAB[e] = need ? fexp(g_of(P, e == 0 ? A : B)) * P.pm : pAB[0];
   }
   wide_fixup(P, A, B, M, pAB[0], pAB[1], lo, hi);

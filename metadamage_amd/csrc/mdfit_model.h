@@ -337,11 +337,11 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
 }
 
 // Cholesky of the free block of H + mu*I (fixed / bound rows -> identity);
-// false if a pivot is not positive.  Packed lower triangle L (same index as
-// H), iL = 1 / diag(L).
-__device__ __forceinline__ bool chol4(const bool fr[4], const double H[10], double mu, double L[10],
-                                      double iL[4]) {
-  bool ok = true;
+// returns the first non-positive pivot's index (-1: positive definite).
+// Packed lower triangle L (same index as H), iL = 1 / diag(L).
+__device__ __forceinline__ int chol4(const bool fr[4], const double H[10], double mu, double L[10],
+                                     double iL[4]) {
+  int jf = -1;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
 #pragma unroll
@@ -352,7 +352,7 @@ __device__ __forceinline__ bool chol4(const bool fr[4], const double H[10], doub
 #pragma unroll
       for (int p = 0; p < m; ++p) s -= L[hidx(p, j)] * L[hidx(p, m)];
       if (j == m) {
-        if (!(s > 0.0)) ok = false;
+        if (!(s > 0.0) && jf < 0) jf = j;
         const double sp = fmax(s, 1e-300);
         const double il = rsqrt_nr(sp);  // 1/L_jj, then L_jj = s/L_jj
         L[hidx(j, j)] = sp * il;
@@ -362,7 +362,7 @@ __device__ __forceinline__ bool chol4(const bool fr[4], const double H[10], doub
       }
     }
   }
-  return ok;
+  return jf;
 }
 
 // Projected, Hessian-modified Newton direction with a Bertsekas binding set
@@ -370,10 +370,8 @@ __device__ __forceinline__ bool chol4(const bool fr[4], const double H[10], doub
 // step onto the bound and leave the Newton system.
 // w = pgnorm(u, g) (the fixed coordinates of model_null have g = 0 and sit
 // inside the box, so they add nothing to it).
-__device__ __forceinline__ void newton_dir(bool pmd, const double u[4], const double g[4],
-                                           const double H[10], double w, double d[4]) {
-  bool fr[4];
-  double dbind[4];
+__device__ __forceinline__ void free_set(bool pmd, const double u[4], const double g[4], const double H[10],
+                                         double w, bool fr[4], double dbind[4]) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const bool fixed = !pmd && (j == 1 || j == 2);
@@ -389,8 +387,43 @@ __device__ __forceinline__ void newton_dir(bool pmd, const double u[4], const do
     dbind[j] = (bind && !fixed) ? (atlo ? kULo[j] : kUHi[j]) - u[j] : 0.0;
     fr[j] = !(fixed || bind);
   }
+}
+
+// Returns true when the free block of H is indefinite (the Cholesky needed a
+// shift): the saddle escape's trigger (oracle: direction()).  With want_nc and
+// an indefinite H, d is instead a direction of non-positive curvature (the
+// saddle escape; oracle: nc_direction): the unshifted Cholesky's first
+// non-positive pivot s_j with the rows above it gives z = (-L^-T l, 1, 0..),
+// z'Hz = s_j <= 0, scaled to max-norm 1 and signed downhill.
+__device__ __forceinline__ bool newton_dir(bool pmd, const double u[4], const double g[4],
+                                           const double H[10], double w, double d[4], bool want_nc = false) {
+  bool fr[4];
+  double dbind[4];
+  free_set(pmd, u, g, H, w, fr, dbind);
   double L[10], iL[4];
-  bool ok = chol4(fr, H, 0.0, L, iL);  // plain Newton: the common case
+  const int jf = chol4(fr, H, 0.0, L, iL);  // plain Newton: the common case
+  const bool indef = jf >= 0;
+  if (want_nc && indef) {
+    double z[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) z[j] = j == jf ? 1.0 : 0.0;
+#pragma unroll
+    for (int p = 2; p >= 0; --p) {
+      if (p < jf) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = p + 1; k < 4; ++k) s += k <= jf ? L[hidx(p, k)] * z[k] : 0.0;  // L(k,p)
+        z[p] = -s * iL[p];
+      }
+    }
+    const double mx = maxabs4(z);
+    const double gz = g[0] * z[0] + g[1] * z[1] + g[2] * z[2] + g[3] * z[3];
+    const double sg = gz > 0.0 ? -1.0 : 1.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d[j] = sg * z[j] / mx;
+    return true;
+  }
+  bool ok = !indef;
   if (!ok) {  // indefinite: shift the diagonal by 1e-10 * scale, x10 per retry
     double sc = 0.0;
 #pragma unroll
@@ -398,7 +431,7 @@ __device__ __forceinline__ void newton_dir(bool pmd, const double u[4], const do
       if (fr[j]) sc = fmax(sc, fabs(H[hidx(j, j)]));
     if (sc == 0.0) sc = 1.0;
     double mu = 1e-10 * sc;
-    for (int attempt = 1; attempt < 40 && !ok; ++attempt, mu *= 10.0) ok = chol4(fr, H, mu, L, iL);
+    for (int attempt = 1; attempt < 40 && !ok; ++attempt, mu *= 10.0) ok = chol4(fr, H, mu, L, iL) < 0;
   }
   if (!ok) {
 #pragma unroll
@@ -428,6 +461,7 @@ __device__ __forceinline__ void newton_dir(bool pmd, const double u[4], const do
 #pragma unroll
     for (int j = 0; j < 4; ++j) d[j] *= 4.0 / mx;
   }
+  return indef;
 }
 
 

@@ -38,7 +38,8 @@
 #define HP_K0 16               /* exact sums this close to a support end */
 #define HP_LV 4.0              /* max panel length in a log variable */
 #define HP_LX 2.5              /* max linear panel length, in units of sd */
-#define HP_STOP 4.0            /* Newton stops when the ends move < this (points) */
+#define HP_STOP 16.0           /* Newton stops when the ends would move < this (counts): the
+                                * exact fix-up walk (~20 instructions a count) finishes */
 
 static const double HP_GLX[3] = {0.2386191860831969, 0.6612093864662645, 0.9324695142031521};
 static const double HP_GLW[3] = {0.4679139345726910, 0.3607615730481386, 0.1713244923791704};
@@ -280,8 +281,12 @@ static void hp_window(double N, double a, double b, double* lo, double* hi) {
     return;
   }
   const double mu = N * a / phi;
-  const double g0 = m > 0 ? hp_g(&P, 0.0) : 0.0;
-  const double gN = m < N ? hp_g(&P, N) : 0.0;
+  /* g(0), g(N) only when that support end is within 4 tau of the mode (tau^2 =
+   * sd^2 + (mean - mode)^2): beyond, the 68 % window (inside mode +- 2.4 tau,
+   * Gauss's inequality) never reaches it */
+  const double tau = sqrt(sd * sd + (mu - m) * (mu - m));
+  const double g0 = m > 0 ? (m <= 4.0 * tau ? hp_g(&P, 0.0) : -INFINITY) : 0.0;
+  const double gN = m < N ? (N - m <= 4.0 * tau ? hp_g(&P, N) : -INFINITY) : 0.0;
   double A, B;
   long double M;
   double t = HP_T0;
@@ -315,7 +320,7 @@ static void hp_window(double N, double a, double b, double* lo, double* hi) {
         xn = N + b - exp(log(N - x + b) - F / dF);
       }
       if (!(lb < xn && xn < hb)) xn = 0.5 * (lb + hb);
-      if (fabs(xn - x) < fmax(HP_STOP, 2e-5 * x) || it >= 40) break;
+      if (fabs(xn - x) < HP_STOP || it >= 40) break;
       x = xn;
     }
   } else {
@@ -359,7 +364,7 @@ static void hp_window(double N, double a, double b, double* lo, double* hi) {
       if (Dp > 0.0) {
         const double Md = (double)M;
         const double dt = (log(Md) - log(HP_MASS)) * Md / Dp;
-        if (fabs(dt) * mv < fmax(HP_STOP, 2e-5 * A)) break;
+        if (fabs(dt) * mv < HP_STOP) break;
         tn = t + dt;
       } else {
         tn = 0.5 * (tL + tH); /* both ends clamped: all the mass, raise the level */

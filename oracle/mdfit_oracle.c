@@ -298,16 +298,21 @@ static void init_u(int model, const uint32_t* y, const uint32_t* N, int lo,
   u[P_C] = c0;
 }
 
+static double maxabs4(const double v[4]) {
+  double m = 0;
+  for (int j = 0; j < 4; j++)
+    if (fabs(v[j]) > m) m = fabs(v[j]);
+  return m;
+}
+
 /* projected, Hessian-modified Newton direction (Bertsekas-style binding set):
  * a variable within eps of a bound whose gradient pushes it outward is moved
  * onto the bound (d = bound - u) and removed from the Newton system; the
  * others take the (Hessian-modified) Newton step of the reduced system. */
 static const double EPS_BIND[4] = {1e-3, 1e-3, 1e-4, 1e-3};
 
-static void direction(int model, const double u[4], const double g[4],
-                      double H[4][4], double d[4]) {
-  int fr[4];
-  double dbind[4] = {0, 0, 0, 0};
+static void free_set(int model, const double u[4], const double g[4], double H[4][4], int fr[4],
+                     double dbind[4]) {
   double w = 0; /* projected-gradient size */
   for (int j = 0; j < 4; j++) {
     if (model == M_NULL && (j == P_A || j == P_C)) continue;
@@ -326,9 +331,17 @@ static void direction(int model, const double u[4], const double g[4],
     double hjj = H[j][j];
     int bind = (atlo && g[j] > -EPS_ACT && (hjj <= 0 || g[j] + EPS_ACT > hjj * dlo)) ||
                (athi && g[j] < EPS_ACT && (hjj <= 0 || -g[j] + EPS_ACT > hjj * dhi));
-    if (bind && !fixed) dbind[j] = (atlo ? U_LO[j] : U_HI[j]) - u[j];
+    dbind[j] = (bind && !fixed) ? (atlo ? U_LO[j] : U_HI[j]) - u[j] : 0.0;
     fr[j] = !(fixed || bind);
   }
+}
+
+/* returns 1 when the free block of H is not positive definite (the Cholesky
+ * needed a shift) */
+static int direction(int model, const double u[4], const double g[4], double H[4][4], double d[4]) {
+  int fr[4];
+  double dbind[4];
+  free_set(model, u, g, H, fr, dbind);
   double sc = 0;
   for (int j = 0; j < 4; j++)
     if (fr[j] && fabs(H[j][j]) > sc) sc = fabs(H[j][j]);
@@ -379,6 +392,48 @@ cap:;
     if (fabs(d[j]) > mx) mx = fabs(d[j]);
   if (mx > 4.0)
     for (int j = 0; j < 4; j++) d[j] *= 4.0 / mx;
+  return mu > 0.0 || !ok;
+}
+
+/* a direction of non-positive curvature of the free block of H (the saddle
+ * escape of fit_one): the unshifted Cholesky's first non-positive pivot s_j
+ * with the computed rows above it gives z = (-L^-T l, 1, 0..), z'Hz = s_j <= 0;
+ * scaled to max-norm 1 and signed downhill.  Returns 0 if H is positive
+ * definite on the free set. */
+static int nc_direction(int model, const double u[4], const double g[4], double H[4][4], double v[4]) {
+  int fr[4];
+  double dbind[4], L[4][4] = {{0}};
+  free_set(model, u, g, H, fr, dbind);
+  int jf = -1;
+  for (int j = 0; j < 4 && jf < 0; j++) {
+    for (int m = 0; m <= j; m++) {
+      double s = (!fr[j] || !fr[m]) ? (j == m ? 1.0 : 0.0) : H[j][m];
+      for (int p = 0; p < m; p++) s -= L[j][p] * L[m][p];
+      if (j == m) {
+        if (!(s > 0)) {
+          jf = j;
+          break;
+        }
+        L[j][j] = sqrt(s);
+      } else {
+        L[j][m] = s / L[m][m];
+      }
+    }
+  }
+  if (jf < 0) return 0;
+  double z[4] = {0, 0, 0, 0};
+  z[jf] = 1.0;
+  for (int p = jf - 1; p >= 0; p--) {
+    double s = 0;
+    for (int k = p + 1; k <= jf; k++) s += L[k][p] * z[k];
+    z[p] = -s / L[p][p];
+  }
+  const double mx = maxabs4(z);
+  double gz = 0;
+  for (int j = 0; j < 4; j++) gz += g[j] * z[j];
+  const double sg = gz > 0 ? -1.0 : 1.0;
+  for (int j = 0; j < 4; j++) v[j] = sg * z[j] / mx;
+  return 1;
 }
 
 /* projected-gradient size max_j |u_j - clamp(u_j - g_j)|: the stationarity
@@ -392,12 +447,6 @@ static double pgnorm(const double u[4], const double g[4]) {
   return m;
 }
 
-static double maxabs4(const double v[4]) {
-  double m = 0;
-  for (int j = 0; j < 4; j++)
-    if (fabs(v[j]) > m) m = fabs(v[j]);
-  return m;
-}
 
 typedef struct {
   double u[4];
@@ -423,20 +472,22 @@ static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
     status = MDFIT_NONFINITE;
     goto done;
   }
-  direction(model, u, cur.g, cur.H, d);
+  int indef = direction(model, u, cur.g, cur.H, d);
   if (maxabs4(d) <= tol) {
     status = MDFIT_OK;
     goto done;
   }
   int rescued = 0, relax = 0; /* the flat-tail rescue (below): once per fit */
+  int nc = 0, n_nc = 0, st_exh = MDFIT_MAXITER; /* the saddle escape (below) */
   while (evals < max_iter) {
     for (int j = 0; j < 4; j++) ut[j] = clampd(u[j] + t * d[j], U_LO[j], U_HI[j]);
     evaluate(model, y, N, lo, hi, ut, &tr);
     evals++;
     const double noise = NOISE_F * (cur.mag + fabs(cur.F));
     int acc = isfinite(tr.F) &&
-              (tr.F < cur.F ||
-               (tr.F <= cur.F + noise && (relax || pgnorm(ut, tr.g) < pgnorm(u, cur.g))));
+              (nc ? tr.F < cur.F - noise
+                  : (tr.F < cur.F ||
+                     (tr.F <= cur.F + noise && (relax || pgnorm(ut, tr.g) < pgnorm(u, cur.g)))));
     relax = 0;
     if (g_trace)
       printf("%d trF=%.12f curF=%.12f acc=%d t=%.3g |d|=%.3e |gt|=%.3e |gc|=%.3e u=[%.10f %.10f %.10f %.10f] d=[%.3e %.3e %.3e %.3e]\n",
@@ -444,10 +495,17 @@ static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
     if (acc) {
       memcpy(u, ut, sizeof(u));
       cur = tr;
-      direction(model, u, cur.g, cur.H, d);
+      indef = direction(model, u, cur.g, cur.H, d);
+      nc = 0;
       t = 1.0;
       if (maxabs4(d) <= tol) {
         status = MDFIT_OK;
+        break;
+      }
+    } else if (nc) { /* the escape step finds no decrease beyond F's rounding */
+      t *= 0.5;
+      if (t < 1e-3) {
+        status = st_exh;
         break;
       }
     } else {
@@ -468,7 +526,24 @@ static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
          * the step's predicted decrease |g.d| is below F's resolution */
         double gd = 0;
         for (int j = 0; j < 4; j++) gd += cur.g[j] * d[j];
-        status = (maxabs4(d) <= 1e-5 || pgnorm(u, cur.g) <= PG_TOL || fabs(gd) <= noise) ? MDFIT_OK : MDFIT_MAXITER;
+        st_exh = (maxabs4(d) <= 1e-5 || pgnorm(u, cur.g) <= PG_TOL || fabs(gd) <= noise) ? MDFIT_OK : MDFIT_MAXITER;
+        /* the saddle escape: at a point whose Hessian is indefinite on the free
+         * set (flat valleys of q, A, c), the shifted Newton step is ~0 and the
+         * line search stalls although F still falls along the negative
+         * curvature.  Up to 4 times per fit: re-evaluate at u (an evaluation,
+         * as the kernel does: it keeps no H), step along nc_direction from t = 1
+         * halving to 1e-3, accepting only a decrease beyond F's rounding. */
+        if (indef && n_nc < 4 && evals < max_iter) {
+          evaluate(model, y, N, lo, hi, u, &tr);
+          evals++;
+          if (nc_direction(model, u, tr.g, tr.H, d)) {
+            n_nc++;
+            nc = 1;
+            t = 1.0;
+            continue;
+          }
+        }
+        status = st_exh;
         break;
       }
     }

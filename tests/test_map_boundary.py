@@ -57,6 +57,26 @@ def test_oracle_subfit_optimum_is_local_min(oracle_lib, subset):
             assert oracle_lib.objective(0, subset, y[i, :30], N[i, :30], v)[0] >= F - noise
 
 
+def test_oracle_escapes_a_saddle(oracle_lib):
+    """Started at the saddle where a GPU fit once stopped (s101_t4066: the
+    Hessian is indefinite there and the gradient ~7e-5, so the shifted Newton
+    step vanishes and the line search is exhausted), the saddle escape steps
+    along the negative curvature and the fit reaches the same optimum as from
+    the spec's initial point, below the saddle by far more than F's rounding."""
+    case = CASES["s101_t4066"]
+    sd = case["saddle"]
+    y, N = np.array(case["y"], np.uint32), np.array(case["N"], np.uint32)
+    u0 = np.array(sd["u"])
+    F0, g0, H0, _ = oracle_lib.objective(sd["model"], sd["subset"], y, N, u0)
+    assert np.linalg.eigvalsh(H0)[0] < 0  # indefinite: a saddle, not a minimum
+    u1, F1, ev1, st1 = oracle_lib.fit_subfit(sd["model"], sd["subset"], y, N, u0=u0)
+    u2, F2, ev2, st2 = oracle_lib.fit_subfit(sd["model"], sd["subset"], y, N)
+    assert st1 == 0 and st2 == 0
+    assert F1 < F0 - 1e-2  # escaped (the saddle is ~0.022 above the optimum)
+    assert abs(F1 - F2) <= 1e-9 * abs(F2)
+    assert np.abs(u1 - u2).max() < 1e-5, (u1, u2)
+
+
 @pytest.mark.gpu
 def test_kernel_converges_at_bounds_like_the_oracle(oracle_lib):
     import torch

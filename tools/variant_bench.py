@@ -62,13 +62,18 @@ def main() -> None:
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.steps
-            out = res.out.cpu().numpy()[:, :25]
+            full = res.out.cpu().numpy()
+            out = full[:, :25]
             st = res.status.cpu().numpy()
             if ref is None:
                 ref = out
-            dev = np.nanmax(np.abs(out - ref) / (np.abs(ref) + 1e-300)) if ref is not None else 0.0
+            rel = np.abs(out - ref) / (np.abs(ref) + 1e-300)
+            dev = np.nanmax(rel)
+            ndiff = int((np.nan_to_num(rel, nan=0.0).max(1) > 1e-9).sum())
+            evals = full[:, _lib.F_DIAG + 5::8][:, :6].sum() if a.mode == "map" else float("nan")
             print(f"rep {rep} {Path(path).name:24s} {ms:8.3f} ms  {a.taxa / ms * 1e3 / 1e6:6.2f} M fits/s  "
-                  f"ok {np.mean(st == 0):.4f}  max rel dev vs first {dev:.1e}", flush=True)
+                  f"ok {np.mean(st == 0):.4f}  max rel dev vs first {dev:.1e} ({ndiff} taxa)  evals {evals:.0f}",
+                  flush=True)
 
 
 if __name__ == "__main__":
