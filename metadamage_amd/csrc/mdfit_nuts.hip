@@ -119,13 +119,23 @@ __device__ __forceinline__ double sel4(const double v[4], int j) {
 
 __device__ __forceinline__ bool active(bool pmd, int j) { return pmd || j == 0 || j == 3; }
 
-// out[j] = v of lane j of this 16-lane row (the row's lanes 0-3 each computed
-// one component of a 4-vector; the row must be converged)
-__device__ __forceinline__ void row4(double v, double out[4]) {
-  out[0] = rowb<0>(v);
-  out[1] = rowb<1>(v);
-  out[2] = rowb<2>(v);
-  out[3] = rowb<3>(v);
+// out[j] = v of lane j of this chain slot (G = 16: a DPP row; G = 8: one half
+// of it) -- the slot's lanes 0-3 each computed one component of a 4-vector;
+// the row must be converged
+template <int G>
+__device__ __forceinline__ void slot4(double v, double out[4]) {
+  if (G == 16) {
+    out[0] = rowb<0>(v);
+    out[1] = rowb<1>(v);
+    out[2] = rowb<2>(v);
+    out[3] = rowb<3>(v);
+  } else {
+    const bool hi8 = threadIdx.x & 8;
+    out[0] = hi8 ? rowb<8>(v) : rowb<0>(v);
+    out[1] = hi8 ? rowb<9>(v) : rowb<1>(v);
+    out[2] = hi8 ? rowb<10>(v) : rowb<2>(v);
+    out[3] = hi8 ? rowb<11>(v) : rowb<3>(v);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -194,6 +204,106 @@ __device__ __forceinline__ Pot potential(const PointData& pd, const double v[4],
   const unsigned long long bm = __ballot(bad_lane);
   const int sh = (int)(threadIdx.x & (whole ? ~31 : ~15));
   const bool bad = ((bm >> sh) & (whole ? 0xFFFFFFFFull : 0xFFFFull)) != 0ull;
+  Pot o;
+  o.U = -(acc[0] + lprior);
+  o.g[0] = -(acc[1] * (q * omq) + (2.0 - 5.0 * q));
+  o.g[1] = pmd ? -(acc[2] * (A * omA) + (2.0 - 5.0 * A)) : 0.0;
+  o.g[2] = pmd ? -(acc[3] * (c * omc) + (1.0 - 10.0 * c)) : 0.0;
+  o.g[3] = -(acc[4] * delta + (1.0 - delta * 1e-3));
+  if (bad || !isfinite(o.U)) {
+    o.U = INFINITY;
+    o.g[0] = o.g[1] = o.g[2] = o.g[3] = 0.0;
+  }
+  return o;
+}
+
+// The same potential in the two-points-per-lane layout (the chain kernel's
+// PPL 2): a pair chain on 8 lanes (lane j: |z|-1 = 2j, 2j+1 of its direction;
+// lane 7's second point the pad), an all-position chain on 16 (lane j: z = +(j+1)
+// and -(j+1); lane 15 the pad).  Lanes 0-3 of each 8-lane half resolve the
+// sigmoids / exp (an all-position chain's halves hold the same v, so both
+// compute the same values); sums over the half, then across halves (whole).
+__device__ __forceinline__ Pot potential2(const PointData pt[2], const double v[4], bool whole) {
+  const int i = (int)(threadIdx.x & 7);
+  const bool hi8 = threadIdx.x & 8;
+  const double x = i < 3 ? sel4(v, i) : v[3];
+  const double e = exp(i < 3 ? -fabs(x) : x);
+  const double sp = flog1p(e);
+  const double rr = rcp(1.0 + e);
+  const bool pos = x >= 0.0;
+  const double p = pos ? rr : e * rr, omp = pos ? e * rr : rr;
+  const double lp = pos ? -sp : x - sp, l1p = pos ? -(x + sp) : -sp;
+  const double pr = i == 2 ? lp + 9.0 * l1p : 2.0 * lp + 3.0 * l1p;
+  auto bc = [=](double y, auto n) {
+    constexpr int N = decltype(n)::value;
+    return hi8 ? rowb<8 + N>(y) : rowb<N>(y);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  const double q = bc(p, I0{}), omq = bc(omp, I0{}), prq = bc(pr, I0{});
+  const double A0 = bc(p, I1{}), omA = bc(omp, I1{}), prA = bc(pr, I1{});
+  const double c0 = bc(p, I2{}), omc = bc(omp, I2{}), prc = bc(pr, I2{});
+  const double delta = bc(e, I3{});
+  const double phi = delta + 2.0;
+  const bool pmd = pt[0].pmd;
+  const double A = pmd ? A0 : 0.0, c = pmd ? c0 : 0.0;
+  double lprior = prq + v[3] - delta * 1e-3;
+  if (pmd) lprior += prA + prc;
+
+  // the pad's lnGamma(0 + phi) pair: lane 7 (pair, forward half) or lane 15
+  const LG3 t3b = lg3<false>(pt[1].N + phi);
+  const bool src15 = whole || hi8;
+  const double t6l = src15 ? rowb<15>(t3b.l) : rowb<7>(t3b.l);
+  const double t6p = src15 ? rowb<15>(t3b.p) : rowb<7>(t3b.p);
+  double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  bool bad_lane = pmd && A + c >= 1.0;
+#ifndef MDFIT_NUTS_PT_UNROLL
+#define MDFIT_NUTS_PT_UNROLL 2
+#endif
+#pragma unroll MDFIT_NUTS_PT_UNROLL
+  for (int pi = 0; pi < 2; ++pi) {
+    const PointData& pd = pt[pi];
+    double D, dq, dA;
+    if (pmd) {
+      const double w = powk(omq, pd.k);
+      D = fma(A, w, c);
+      dq = pd.k > 0 ? -A * (double)pd.k * (w * rcp(omq)) : 0.0;
+      dA = w;
+    } else {
+      D = q;
+      dq = 1.0;
+      dA = 0.0;
+    }
+    bad_lane = bad_lane || (pd.valid && !(D < 1.0));
+    const double a = D * phi, b = (1.0 - D) * phi;
+    const LG3 t1 = lg3<false>(pd.y + a);
+    const LG3 t4 = lg3<false>(a);
+    const double la = t1.l - t4.l, Pa = t1.p - t4.p;
+    const LG3 t2 = lg3<false>(pd.N - pd.y + b);
+    const LG3 t5 = lg3<false>(b);
+    const double lb = t2.l - t5.l, Pb = t2.p - t5.p;
+    const LG3 t3 = pi == 1 ? t3b : lg3<false>(pd.N + phi);
+    const double ell = (la + lb) - (t3.l - t6l);
+    const double lD = phi * (Pa - Pb);
+    const double lF = D * Pa + (1.0 - D) * Pb + (t6p - t3.p);
+    if (pd.valid) {
+      acc[0] += ell;
+      acc[1] += lD * dq;
+      acc[2] += lD * dA;
+      acc[3] += lD;
+      acc[4] += lF;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    const double s8 = gsum<8>(acc[j]);
+    acc[j] = whole ? s8 + dpp<0x140>(s8) : s8;  // row_mirror: the other half's sum
+  }
+  const unsigned long long bm = __ballot(bad_lane);
+  const int sh = (int)(threadIdx.x & (whole ? ~15 : ~7));
+  const bool bad = ((bm >> sh) & (whole ? 0xFFFFull : 0xFFull)) != 0ull;
   Pot o;
   o.U = -(acc[0] + lprior);
   o.g[0] = -(acc[1] * (q * omq) + (2.0 - 5.0 * q));
@@ -353,28 +463,51 @@ constexpr int kInit = 1, kFind = 2, kIter = 3, kDone = 4;
 // ---------------------------------------------------------------------------
 // chain kernel
 // ---------------------------------------------------------------------------
+// Chain layouts (template PPL = points per lane): a task group of 2 chain
+// slots runs one all-position chain (both slots hold identical state, their
+// sums added) or the forward / reverse pair of one model (a chain per slot).
+//   PPL 1: slot = a 16-lane DPP row, lane = position (lane 15 the pad);
+//          2 task groups / 4 chain slots per wave.
+//   PPL 2: slot = 8 lanes, two positions per lane (pair: |z|-1 = 2j, 2j+1;
+//          all-position: z = +-(j+1) on 16 lanes); 4 task groups / 8 chain
+//          slots per wave -- every state-machine pass serves twice the chains.
 #ifndef MDFIT_NUTS_WAVES_PER_EU
-#define MDFIT_NUTS_WAVES_PER_EU 3  // register budget per lane: 512 / waves (VGPR+AGPR); 3 measured best (C3)
+#define MDFIT_NUTS_WAVES_PER_EU 3  // PPL 1 register budget per lane: 512 / waves (VGPR+AGPR); 3 measured best (C3)
 #endif
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUTS_WAVES_PER_EU))) void nuts_chain_kernel(const uint32_t* __restrict__ gy,
+#ifndef MDFIT_NUTS_WAVES_PER_EU2
+#define MDFIT_NUTS_WAVES_PER_EU2 2  // PPL 2 (LDS: ~13.5 KB of chain state per wave)
+#endif
+#ifndef MDFIT_NUTS_PPL
+#define MDFIT_NUTS_PPL 1
+#endif
+template <int PPL>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PPL == 1 ? MDFIT_NUTS_WAVES_PER_EU : MDFIT_NUTS_WAVES_PER_EU2))) void nuts_chain_kernel(const uint32_t* __restrict__ gy,
                                                            const uint32_t* __restrict__ gN, int64_t T,
                                                            mdfit_opts o, double* __restrict__ out,
                                                            int* __restrict__ ws, double* __restrict__ samples) {
-  __shared__ RowState srow[4];
-  __shared__ ChainState schain[4];
-  __shared__ double sck[8][kWave];  // checkpoint i of a row on its lane i: r[4], rsum[4]
-  // draws of the current iteration computed one per lane, in parallel: lane j
-  // of a row holds doubling j's direction bit and subtree-merge uniform, and
-  // leaf uniform 16 c + j of the current chunk c (ChainState::ul_chunk)
-  __shared__ double sut[kWave], sul[kWave];
-  // momenta of 4 iterations: lane i of a row holds component i & 3 of
-  // iteration 4 c + (i >> 2), c = ChainState::nm_chunk
-  __shared__ double snm[kWave];
-  __shared__ int sdb[kWave];
+  static_assert(PPL == 1 || PPL == 2, "points per lane");
+  constexpr int kG = PPL == 1 ? 16 : 8;  // lanes per chain slot
+  constexpr int kNSlot = kWave / kG;     // chain slots per wave
+  constexpr int kTaskL = 2 * kG;         // lanes per task group
+  constexpr unsigned long long kTaskMask = kTaskL == 32 ? 0xFFFFFFFFull : 0xFFFFull;
+  constexpr unsigned long long kSlotMask = kG == 16 ? 0xFFFFull : 0xFFull;
+  __shared__ RowState srow[kNSlot];
+  __shared__ ChainState schain[kNSlot];
+  __shared__ double sck[8][kWave];  // checkpoint i of a slot on its lane i: r[4], rsum[4]
+  __shared__ double sck8[PPL == 2 ? kNSlot : 1][8];  // PPL 2: checkpoint 8 of a slot
+  // draws of the current iteration computed in parallel, 16 per slot (16 / kG
+  // per lane): entry j holds doubling j's direction bit and subtree-merge
+  // uniform, and leaf uniform 16 c + j of the current chunk c
+  // (ChainState::ul_chunk)
+  __shared__ double sut[16 * kNSlot], sul[16 * kNSlot];
+  // momenta of 4 iterations: entry e of a slot holds component e & 3 of
+  // iteration 4 c + (e >> 2), c = ChainState::nm_chunk
+  __shared__ double snm[16 * kNSlot];
+  __shared__ int sdb[16 * kNSlot];
   const int lane = threadIdx.x;
-  const int r = lane & 31, h = r >> 4, i = r & 15, row = lane >> 4;
-  const int row16 = lane & ~15;
-  const int leader = lane & ~31;
+  const int r = lane & (kTaskL - 1), h = r / kG, i = r & (kG - 1), row = lane / kG;
+  const int row16 = row * 16;  // the slot's 16 entries of the draw caches
+  const int leader = lane & ~(kTaskL - 1);
   const int qi = blockIdx.x % kQueues;
   // queue qi owns the taxa [tl, tl + nq) and serves their 4 nq tasks heaviest
   // kind first: PMD all-position chains, PMD fwd/rev pairs, null all-position,
@@ -384,11 +517,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   RowState& R = srow[row];
   ChainState& C = schain[row];
 
-  PointData pd;
-  pd.valid = i < kNHalf;
-  pd.k = pd.valid ? i : 0;
-  pd.y = pd.N = 0.0;
-  pd.pmd = true;
+  PointData pd[PPL];
+#pragma unroll
+  for (int p = 0; p < PPL; ++p) {
+    pd[p].valid = PPL == 1 ? i < kNHalf : 0;
+    pd[p].k = PPL == 1 && i < kNHalf ? i : 0;
+    pd[p].y = pd[p].N = 0.0;
+    pd[p].pmd = true;
+  }
 
   // The chain state is row-uniform (every lane of a row holds the same values;
   // both rows of an all-position chain too) and lives in LDS, so the
@@ -440,6 +576,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   double& st_leap = C.st_leap;
   chain_init(C);  // every lane of the row writes the same values
   for (int j = 0; j < 8; ++j) sck[j][lane] = 0.0;
+  if (PPL == 2 && i == 0)
+    for (int j = 0; j < 8; ++j) sck8[row][j] = 0.0;
   // the adaptation schedule depends on num_warmup only: window ends once per
   // wave (lane w < 16 resolves window w) instead of once per transition
   __shared__ int swin_end[kMaxWin];
@@ -496,7 +634,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
 #endif
     // ---- 1. free groups start a task (one atomic per wave-trip) --------------
     const unsigned long long busy_m = __ballot(mode != 0 && mode != kDone);
-    const bool group_free = ((busy_m >> leader) & 0xFFFFFFFFull) == 0ull;
+    const bool group_free = ((busy_m >> leader) & kTaskMask) == 0ull;
     if (group_free) mode = 0;  // both chains finished (or none started)
     const bool need = group_free && !drained;
     bool starting = false;
@@ -520,12 +658,27 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       }
     }
     if (starting) {
-      pd.pmd = sub == 0 || sub == 2 || sub == 3;
-      // row h reads columns h*15 + k: the two halves of an all-position chain,
-      // or the forward (sub 2 / 4) / reverse (sub 3 / 5) chain of a pair
-      const int colv = pd.valid ? h * kNHalf + pd.k : 0;
-      pd.y = pd.valid ? (double)gy[taxon * kLD + colv] : 0.0;
-      pd.N = pd.valid ? (double)gN[taxon * kLD + colv] : 0.0;
+      const int pmd_task = sub == 0 || sub == 2 || sub == 3;
+#pragma unroll
+      for (int p = 0; p < PPL; ++p) {
+        pd[p].pmd = pmd_task;
+        int colv;
+        if (PPL == 1) {
+          // row h reads columns h*15 + k: the two halves of an all-position
+          // chain, or the forward (sub 2 / 4) / reverse (sub 3 / 5) chain of a pair
+          colv = h * kNHalf + pd[p].k;
+        } else if (whole) {  // lane r: z = +(r+1) (p 0) and -(r+1) (p 1)
+          pd[p].valid = r < kNHalf;
+          pd[p].k = r < kNHalf ? r : 0;
+          colv = p * kNHalf + pd[p].k;
+        } else {  // lane i of half h: |z|-1 = 2i + p of direction h
+          pd[p].valid = 2 * i + p < kNHalf;
+          pd[p].k = pd[p].valid ? 2 * i + p : 0;
+          colv = h * kNHalf + pd[p].k;
+        }
+        pd[p].y = pd[p].valid ? (double)gy[taxon * kLD + colv] : 0.0;
+        pd[p].N = pd[p].valid ? (double)gN[taxon * kLD + colv] : 0.0;
+      }
       st = make_stream(o.seed, o.index_base + taxon, sub);
       C.nm_chunk = -1;
       // fresh chain state (oracle: nuts_chain)
@@ -540,7 +693,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       t_da = widx = wn = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        pz[j] = active(pd.pmd, j) ? -2.0 + 4.0 * uniform(st, 0xFFFF0000u, (uint32_t)j) : 0.0;
+        pz[j] = active(pd[0].pmd, j) ? -2.0 + 4.0 * uniform(st, 0xFFFF0000u, (uint32_t)j) : 0.0;
         pr[j] = pg[j] = 0.0;
         invm[j] = isd[j] = 1.0;
         R.wmean[j] = R.wm2[j] = 0.0;
@@ -562,11 +715,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
     double zev2[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) zev2[j] = zev[j] * (1.0 + 1e-300 * (double)it);
-    const Pot P0 = potential(pd, zev2, whole);
-    Pot P = potential(pd, zev, whole);
+    const Pot P0 = PPL == 1 ? potential(pd[0], zev2, whole) : potential2(pd, zev2, whole);
+    Pot P = PPL == 1 ? potential(pd[0], zev, whole) : potential2(pd, zev, whole);
     P.U += 0.0 * P0.U * (double)(it > (1 << 30));
 #else
-    const Pot P = potential(pd, zev, whole);
+    const Pot P = PPL == 1 ? potential(pd[0], zev, whole) : potential2(pd, zev, whole);
 #endif
     NSTAMP(2);
     if (!running) continue;
@@ -591,7 +744,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         begin_find = true;
       } else if (++attempt >= 100) {
         // no finite initial point: NaN draws, status 2
-        for (int s = i; s < S; s += 16)
+        for (int s = i; s < S; s += kG)
           if (!whole || h == 0)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
@@ -604,10 +757,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          pz[j] = active(pd.pmd, j) ? -2.0 + 4.0 * uniform(st, 0xFFFF0000u + (uint32_t)attempt, (uint32_t)j) : 0.0;
+          pz[j] = active(pd[0].pmd, j) ? -2.0 + 4.0 * uniform(st, 0xFFFF0000u + (uint32_t)attempt, (uint32_t)j) : 0.0;
       }
     } else if (mode == kFind) {
-      const double de = (P.U + kinetic(pd.pmd, invm, rn)) - e0;
+      const double de = (P.U + kinetic(pd[0].pmd, invm, rn)) - e0;
       const int dnew = log(kTarget) < -de ? 1 : -1;
       f_last = f_dir;
       f_dir = dnew;
@@ -624,7 +777,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       }
     } else {  // kIter: a leaf of the subtree
       ++nleap;
-      double de = (P.U + kinetic(pd.pmd, invm, rn)) - e0;
+      double de = (P.U + kinetic(pd[0].pmd, invm, rn)) - e0;
       if (isnan(de)) de = INFINITY;
       const double w = -de;
       const bool dv = de > kMaxDelta;
@@ -647,8 +800,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         const double e = exp(-fabs(s_w - w));
         const double nw = m == -INFINITY ? -INFINITY : m + flog1p(e);
         const double prob = (w >= s_w ? 1.0 : e) * rcp(1.0 + e);
-        if ((leaf_ctr >> 4) != ul_chunk) {  // next 16 leaf uniforms, one per lane
-          sul[lane] = uniform(st, (uint32_t)it, 32u + (uint32_t)(leaf_ctr & ~15) + (uint32_t)i);
+        if ((leaf_ctr >> 4) != ul_chunk) {  // next 16 leaf uniforms, 16 / kG per lane
+#pragma unroll
+          for (int e2 = 0; e2 < 16 / kG; ++e2) {
+            const int ix = i + kG * e2;
+            sul[row16 + ix] = uniform(st, (uint32_t)it, 32u + (uint32_t)(leaf_ctr & ~15) + (uint32_t)ix);
+          }
           ul_chunk = leaf_ctr >> 4;
         }
         if (sul[row16 + (leaf_ctr & 15)] < prob) {
@@ -670,11 +827,20 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       ++leaf_ctr;
       int imin, imax;
       ckpt_idxs(n_leaf, &imin, &imax);
+      // checkpoint ix (0..8) on lane ix of the slot (PPL 2: checkpoint 8 in
+      // sck8, lane 0)
       if ((n_leaf & 1) == 0 && i == imax) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           sck[j][lane] = rn[j];
           sck[4 + j][lane] = s_rsum[j];
+        }
+      }
+      if (PPL == 2 && (n_leaf & 1) == 0 && imax == 8 && i == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          sck8[row][j] = rn[j];
+          sck8[row][4 + j] = s_rsum[j];
         }
       }
       bool my_turn = false;
@@ -685,10 +851,19 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
           ck_r[j] = sck[j][lane];
           sub_rsum[j] = s_rsum[j] - sck[4 + j][lane] + ck_r[j];
         }
-        my_turn = is_turning(pd.pmd, invm, ck_r, rn, sub_rsum);
+        my_turn = is_turning(pd[0].pmd, invm, ck_r, rn, sub_rsum);
+      }
+      if (PPL == 2 && i == 0 && imin <= 8 && imax >= 8) {
+        double ck_r[4], sub_rsum[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          ck_r[j] = sck8[row][j];
+          sub_rsum[j] = s_rsum[j] - sck8[row][4 + j] + ck_r[j];
+        }
+        my_turn = my_turn || is_turning(pd[0].pmd, invm, ck_r, rn, sub_rsum);
       }
       const unsigned long long tm = __ballot(my_turn);
-      const bool s_turn = ((tm >> (lane & ~15)) & 0xFFFFull) != 0ull;
+      const bool s_turn = ((tm >> (lane & ~(kG - 1))) & kSlotMask) != 0ull;
       ++n_leaf;
 #pragma unroll
       for (int j = 0; j < 4; ++j) pr[j] = rn[j];
@@ -729,7 +904,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) t_rsum[j] += s_rsum[j];
-        t_turn = s_turn || (right ? is_turning(pd.pmd, invm, olr, pr, t_rsum) : is_turning(pd.pmd, invm, pr, olr, t_rsum));
+        t_turn = s_turn || (right ? is_turning(pd[0].pmd, invm, olr, pr, t_rsum) : is_turning(pd[0].pmd, invm, pr, olr, t_rsum));
         t_div = s_div;
         t_acc += s_acc;
         t_n += s_n;
@@ -755,7 +930,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
               ++wn;
 #pragma unroll
               for (int j = 0; j < 4; ++j) {
-                if (!active(pd.pmd, j)) continue;
+                if (!active(pd[0].pmd, j)) continue;
                 const double d0 = R.tz[j] - R.wmean[j];
                 R.wmean[j] += d0 / wn;
                 R.wm2[j] += d0 * (R.tz[j] - R.wmean[j]);
@@ -765,7 +940,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
             if (at_end && middle) {
 #pragma unroll
               for (int j = 0; j < 4; ++j) {
-                if (!active(pd.pmd, j)) continue;
+                if (!active(pd[0].pmd, j)) continue;
                 const double var = R.wm2[j] / (wn - 1);
                 invm[j] = ((double)wn / (wn + 5.0)) * var + 1e-3 * (5.0 / (wn + 5.0));
                 isd[j] = sqrt(1.0 / invm[j]);
@@ -781,7 +956,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
             if ((!whole || h == 0) && i < 4) {
               const double zj = R.tz[i];
               samples[sidx + i] = i == 3 ? exp(zj) + 2.0
-                                         : ((i == 0 || pd.pmd) ? 1.0 / (1.0 + exp(-zj)) : 0.0);
+                                         : ((i == 0 || pd[0].pmd) ? 1.0 / (1.0 + exp(-zj)) : 0.0);
             }
             st_div += t_div ? 1.0 : 0.0;
             st_leap += (double)nleap;
@@ -828,14 +1003,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       eps = ldexp(eps, f_dir);
       // the 4 momentum draws in parallel: lane j of the row draws component j
       double nj[4];
-      row4(normal(st, 0xFFFE0000u + 4096u * (uint32_t)f_call + (uint32_t)f_m, (uint32_t)(i & 3)), nj);
+      slot4<kG>(normal(st, 0xFFFE0000u + 4096u * (uint32_t)f_call + (uint32_t)f_m, (uint32_t)(i & 3)), nj);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        pr[j] = active(pd.pmd, j) ? nj[j] * isd[j] : 0.0;
+        pr[j] = active(pd[0].pmd, j) ? nj[j] * isd[j] : 0.0;
         pz[j] = R.tz[j];
         pg[j] = R.tg[j];
       }
-      e0 = R.tpe + kinetic(pd.pmd, invm, pr);
+      e0 = R.tpe + kinetic(pd[0].pmd, invm, pr);
       step = eps;
     }
     if (begin_iter) {
@@ -843,7 +1018,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       // this iteration's momenta from the 4-iteration cache (the same draws,
       // keyed by iteration and component; one Box-Muller pass per 4 iterations)
       if ((it >> 2) != C.nm_chunk) {
-        snm[lane] = normal(st, (uint32_t)((it & ~3) + (i >> 2)), (uint32_t)(i & 3));
+#pragma unroll
+        for (int e2 = 0; e2 < 16 / kG; ++e2) {
+          const int ix = i + kG * e2;
+          snm[row16 + ix] = normal(st, (uint32_t)((it & ~3) + (ix >> 2)), (uint32_t)(ix & 3));
+        }
         C.nm_chunk = it >> 2;
       }
       double nj[4];
@@ -851,7 +1030,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       for (int j = 0; j < 4; ++j) nj[j] = snm[row16 + 4 * (it & 3) + j];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        pr[j] = active(pd.pmd, j) ? nj[j] * isd[j] : 0.0;
+        pr[j] = active(pd[0].pmd, j) ? nj[j] * isd[j] : 0.0;
         pz[j] = R.tz[j];
         pg[j] = R.tg[j];
         R.lz[j] = R.rz[j] = pz[j];
@@ -859,7 +1038,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         R.lg[j] = R.rg[j] = pg[j];
         t_rsum[j] = pr[j];
       }
-      e0 = R.tpe + kinetic(pd.pmd, invm, pr);
+      e0 = R.tpe + kinetic(pd[0].pmd, invm, pr);
       t_w = 0.0;
       t_acc = 0.0;
       t_n = 0;
@@ -868,8 +1047,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       leaf_ctr = 0;
       nleap = 0;
       // this iteration's doubling draws, lane j of the row for depth j
-      sdb[lane] = (int)(block(st, (uint32_t)it, 4u + 2u * (uint32_t)i).x & 1u);
-      sut[lane] = uniform(st, (uint32_t)it, 5u + 2u * (uint32_t)i);
+#pragma unroll
+      for (int e2 = 0; e2 < 16 / kG; ++e2) {
+        const int ix = i + kG * e2;
+        sdb[row16 + ix] = (int)(block(st, (uint32_t)it, 4u + 2u * (uint32_t)ix).x & 1u);
+        sut[row16 + ix] = uniform(st, (uint32_t)it, 5u + 2u * (uint32_t)ix);
+      }
       ul_chunk = -1;
       right = sdb[row16] != 0;
       u_tr = sut[row16];
@@ -1225,19 +1408,37 @@ __global__ __launch_bounds__(kWave) void nuts_potential_kernel(const int32_t* __
                                                                double* __restrict__ U, double* __restrict__ g) {
   const int64_t it = blockIdx.x;
   if (it >= n) return;
-  const int lane = threadIdx.x, r = lane & 31, h = r >> 4, k = r & 15;
+  const int lane = threadIdx.x;
   const bool whole = subset[it] == 0;
-  PointData pd;
-  pd.pmd = model[it] == 0;
-  pd.valid = (whole ? lane < 32 : lane < 16) && k < kNHalf;
-  pd.k = pd.valid ? k : 0;
-  const int col = pd.valid ? (whole ? h : (subset[it] == 2 ? 1 : 0)) * kNHalf + k : 0;
-  pd.y = pd.valid ? (double)gy[it * kLD + col] : 0.0;
-  pd.N = pd.valid ? (double)gN[it * kLD + col] : 0.0;
+  const int dir = subset[it] == 2 ? 1 : 0;
   double v[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) v[j] = gv[it * 4 + j];
-  const Pot P = potential(pd, v, whole);
+  Pot P;
+  if (MDFIT_NUTS_PPL == 1) {
+    const int r = lane & 31, h = r >> 4, k = r & 15;
+    PointData pd;
+    pd.pmd = model[it] == 0;
+    pd.valid = (whole ? lane < 32 : lane < 16) && k < kNHalf;
+    pd.k = pd.valid ? k : 0;
+    const int col = pd.valid ? (whole ? h : dir) * kNHalf + k : 0;
+    pd.y = pd.valid ? (double)gy[it * kLD + col] : 0.0;
+    pd.N = pd.valid ? (double)gN[it * kLD + col] : 0.0;
+    P = potential(pd, v, whole);
+  } else {  // the chain kernel's PPL 2 layout on lanes 0-15 (whole) or 0-7
+    PointData pd[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      pd[p].pmd = model[it] == 0;
+      const int k = whole ? (lane & 15) : 2 * (lane & 7) + p;
+      pd[p].valid = (whole ? lane < 16 : lane < 8) && k < kNHalf;
+      pd[p].k = pd[p].valid ? k : 0;
+      const int col = pd[p].valid ? (whole ? p : dir) * kNHalf + k : 0;
+      pd[p].y = pd[p].valid ? (double)gy[it * kLD + col] : 0.0;
+      pd[p].N = pd[p].valid ? (double)gN[it * kLD + col] : 0.0;
+    }
+    P = potential2(pd, v, whole);
+  }
   if (lane == 0) {
     U[it] = P.U;
 #pragma unroll
@@ -1269,9 +1470,11 @@ int fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t 
   // diag slots 4..7 are written by the chains; zero the record first
   if (hipMemsetAsync(out, 0, (size_t)n_taxa * MDFIT_NOUT * sizeof(double), s) != hipSuccess)
     return host::check_launch("hipMemsetAsync(out)");
-  const int64_t g = host::fit_grid(nuts_chain_kernel, 4 * n_taxa, 2);
+  constexpr int kPPL = MDFIT_NUTS_PPL;
+  const int64_t g = host::fit_grid(nuts_chain_kernel<kPPL>, 4 * n_taxa, kPPL == 1 ? 2 : 4);
   host::prof_mark(1, s);
-  hipLaunchKernelGGL(nuts_chain_kernel, dim3((unsigned)g), dim3(kWave), 0, s, y, N, n_taxa, o, out, ws, samples);
+  hipLaunchKernelGGL(nuts_chain_kernel<kPPL>, dim3((unsigned)g), dim3(kWave), 0, s, y, N, n_taxa, o, out, ws,
+                     samples);
   if (int rc = host::check_launch("nuts_chain_kernel")) return rc;
   host::prof_mark(2, s);
   size_t sv_bytes = sizeof(double);
