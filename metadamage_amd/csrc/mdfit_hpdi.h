@@ -55,7 +55,10 @@ __device__ unsigned long long g_hpdi_cnt[32];
 #endif
 
 constexpr double kMass = 0.68;
-constexpr double kSigGreedy = 100.0;
+#ifndef MDFIT_HPDI_SIG_GREEDY
+#define MDFIT_HPDI_SIG_GREEDY 100.0
+#endif
+constexpr double kSigGreedy = MDFIT_HPDI_SIG_GREEDY;
 constexpr double kT0 = -0.49447329849;  // -Z68^2 / 2
 constexpr double kK0 = 16.0;
 constexpr double kLV = 4.0;

@@ -33,7 +33,9 @@
  */
 
 #define HP_MASS 0.68
-#define HP_SIG_GREEDY 100.0
+#ifndef HP_SIG_GREEDY
+#define HP_SIG_GREEDY 100.0 /* sd (counts) up to which the greedy itself runs */
+#endif
 #define HP_T0 (-0.49447329849) /* -Z68^2 / 2: the Gaussian 68 % level */
 #define HP_K0 16               /* exact sums this close to a support end */
 #define HP_LV 4.0              /* max panel length in a log variable */
