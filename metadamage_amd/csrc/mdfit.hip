@@ -781,18 +781,45 @@ __global__ __launch_bounds__(kWave) void hpdi_prep_kernel(HpdiIO io, int64_t n_i
   }
 }
 
-// one lane per wide window; the records are in K4a's append order, so a wave's
-// lanes mostly hold neighbouring positions of the same taxa (similar work)
+// one lane per wide window at a time: every trip each busy lane runs one level
+// iteration of its window; a settled window is finished (fix-up, write) and
+// the lane claims the next record (one atomic per wave-trip on ctr[1]), so the
+// wave's evaluation sites stay busy whatever each window's iteration count.
+// Exit: a lane that draws an index past the list stops claiming; the wave
+// leaves when none of its lanes holds a window.
 template <bool kFit>
-__global__ __launch_bounds__(kWave) void hpdi_wide_kernel(HpdiIO io, const int* __restrict__ ctr,
+__global__ __launch_bounds__(kWave) void hpdi_wide_kernel(HpdiIO io, int* __restrict__ ctr,
                                                           const hpdi::WideRec* __restrict__ recs) {
   const int n_wide = ctr[0];  // written by K4a (stream-ordered)
-  for (int64_t i = (int64_t)blockIdx.x * kWave + threadIdx.x; i < n_wide; i += (int64_t)gridDim.x * kWave) {
-    const hpdi::WideRec r = recs[i];
-    HPDI_CNT(8);
-    double lo, hi;
-    hpdi::wide_window(r, lo, hi);
-    hpdi_write<kFit>(io, r.item, r.N, lo, hi);
+  hpdi::Wide W;
+  int64_t item = 0;
+  bool busy = false, drained = false;
+  while (true) {
+    const bool need = !busy && !drained;
+    const unsigned long long m = __ballot(need);
+    if (m != 0ull) {
+      int base = 0;
+      if (threadIdx.x == 0) base = atomicAdd(ctr + 1, __popcll(m));
+      base = __shfl(base, 0);
+      if (need) {
+        const int idx = base + __popcll(m & ((1ull << threadIdx.x) - 1ull));
+        if (idx < n_wide) {
+          const hpdi::WideRec r = recs[idx];
+          item = r.item;
+          hpdi::wide_start(W, r);
+          busy = true;
+        } else {
+          drained = true;
+        }
+      }
+    }
+    if (!__any(busy)) break;
+    if (busy && hpdi::wide_iter(W)) {
+      double lo, hi;
+      hpdi::wide_finish(W, lo, hi);
+      hpdi_write<kFit>(io, item, W.P.N, lo, hi);
+      busy = false;
+    }
   }
 }
 

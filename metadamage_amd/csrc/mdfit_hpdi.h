@@ -414,10 +414,27 @@ __device__ __forceinline__ void wide_fixup(const Pmf& P, double A, double B, dou
   hi = B;
 }
 
-__device__ __forceinline__ void wide_window(const WideRec& r, double& lo, double& hi) {
+// A wide window's state between level iterations: K4b's lanes run one
+// iteration per trip and refill with the next window when theirs is settled,
+// so a wave's evaluation sites stay busy whatever each window's iteration
+// count (the per-window arithmetic is the straight-line sequence of the
+// oracle's hp_window; the order windows are processed in changes nothing).
+struct Wide {
   Pmf P;
-  load_pmf(P, r);
-  const double N = P.N, m = P.m, sd = r.sd, mu = r.mu;
+  double sd, mu, g0, gN;
+  double t, tL, tH;     // two-sided: the level and its bracket
+  double x, lb, hb;     // one-sided: the free end and its bracket
+  double xe0, xe1;      // two-sided: the ends (root starts)
+  double A, B, M;       // the current window and its mass
+  int one, it;
+};
+
+__device__ __forceinline__ void wide_start(Wide& W, const WideRec& r) {
+  HPDI_CNT(8);
+  load_pmf(W.P, r);
+  const double N = W.P.N, m = W.P.m, sd = r.sd, mu = r.mu;
+  W.sd = sd;
+  W.mu = mu;
   // g(0), g(N) (one site) only when that end is within 4 tau of the mode
   const double tau = sqrt(sd * sd + (mu - m) * (mu - m));
   double gE[2];
@@ -426,120 +443,145 @@ __device__ __forceinline__ void wide_window(const WideRec& r, double& lo, double
     const bool inside = e == 0 ? m > 0.0 : m < N;
     const bool near = (e == 0 ? m : N - m) <= 4.0 * tau;
     if (inside && near) HPDI_CNT(0);
-    gE[e] = inside ? (near ? g_of(P, e == 0 ? 0.0 : N) : -INFINITY) : 0.0;
+    gE[e] = inside ? (near ? g_of(W.P, e == 0 ? 0.0 : N) : -INFINITY) : 0.0;
   }
-  const double g0 = gE[0], gN = gE[1];
-  double t = kT0;
-  const bool L0 = m == 0.0 || g0 >= t, R0 = m == N || gN >= t;
-  const int one = (L0 && !R0) ? 0 : ((R0 && !L0) ? 1 : -1);
-  double x = one == 0 ? fmax(mu, m + 1.0) : fmin(mu, m - 1.0);
-  double lb = one == 0 ? m : 0.0, hb = one == 0 ? N : m;
-  double tL = -INFINITY, tH = 0.0;
-  double xe[2] = {m - sd, m + sd};  // two-sided ends
-  double A = m, B = m, M = P.pm;
-  for (int it = 0;; ++it) {
-    HPDI_CNT(9);
-    bool cl = false, cr = false;
-    if (one < 0) {
-      cl = m == 0.0 || g0 >= t;
-      cr = m == N || gN >= t;
-      // the free ends' roots of g = t (oracle: hp_root): one site for both
-#pragma unroll 1
-      for (int e = 0; e < 2; ++e) {
-        const bool clamped = e == 0 ? cl : cr;
-        if (clamped) {
-          xe[e] = e == 0 ? 0.0 : N;
-          continue;
-        }
-        double rlo = e == 0 ? 0.0 : m, rhi = e == 0 ? m : N;
-        const bool rising = e == 0;
-        double xr = fmin(fmax(xe[e], rlo), rhi);
-        for (int k = 0; k < 60; ++k) {
-          double sx;
-          HPDI_CNT(1);
-          const double gx = gfun<true>(P, xr, sx) - t;
-          if (fabs(gx) < 1e-12) break;
-          if ((gx < 0.0) == rising) rlo = xr;
-          else rhi = xr;
-          double xn = sx != 0.0 ? xr - gx / sx : 0.5 * (rlo + rhi);
-          if (!(rlo < xn && xn < rhi)) xn = 0.5 * (rlo + rhi);
-          const bool conv = fabs(xn - xr) < 0.05;
-          xr = xn;
-          if (conv) break;
-        }
-        xe[e] = xr;
-      }
-      A = ceil(xe[0]);
-      B = floor(xe[1]);
-    } else {
-      A = one == 0 ? 0.0 : ceil(x);
-      B = one == 0 ? floor(x) : N;
-    }
-    M = wide_mass(P, A, B, sd) * P.pm;
-    // the evaluations after the mass: f(x) (one-sided) or s at the two ends
-    double pe[2] = {0.0, 0.0};
+  W.g0 = gE[0];
+  W.gN = gE[1];
+  W.t = kT0;
+  const bool L0 = m == 0.0 || W.g0 >= W.t, R0 = m == N || W.gN >= W.t;
+  W.one = (L0 && !R0) ? 0 : ((R0 && !L0) ? 1 : -1);
+  W.x = W.one == 0 ? fmax(mu, m + 1.0) : fmin(mu, m - 1.0);
+  W.lb = W.one == 0 ? m : 0.0;
+  W.hb = W.one == 0 ? N : m;
+  W.tL = -INFINITY;
+  W.tH = 0.0;
+  W.xe0 = m - sd;  // two-sided ends
+  W.xe1 = m + sd;
+  W.A = W.B = m;
+  W.M = W.P.pm;
+  W.it = 0;
+}
+
+// one level iteration (oracle: hp_window's loop body); true when settled
+__device__ __forceinline__ bool wide_iter(Wide& W) {
+  HPDI_CNT(9);
+  const Pmf& P = W.P;
+  const double N = P.N, m = P.m;
+  const int one = W.one, it = W.it;
+  const double t = W.t;
+  double A, B;
+  double xe[2] = {W.xe0, W.xe1};
+  bool cl = false, cr = false;
+  if (one < 0) {
+    cl = m == 0.0 || W.g0 >= t;
+    cr = m == N || W.gN >= t;
+    // the free ends' roots of g = t (oracle: hp_root): one site for both
 #pragma unroll 1
     for (int e = 0; e < 2; ++e) {
-      const bool need = one >= 0 ? e == 0 : (e == 0 ? !cl : !cr);
-      if (!need) continue;
-      double sx;
-      HPDI_CNT(4);
-      const double gx = gfun<true>(P, one >= 0 ? x : xe[e], sx);
-      pe[e] = one >= 0 ? fexp(gx) * P.pm : sx;
+      const bool clamped = e == 0 ? cl : cr;
+      if (clamped) {
+        xe[e] = e == 0 ? 0.0 : N;
+        continue;
+      }
+      double rlo = e == 0 ? 0.0 : m, rhi = e == 0 ? m : N;
+      const bool rising = e == 0;
+      double xr = fmin(fmax(xe[e], rlo), rhi);
+      for (int k = 0; k < 60; ++k) {
+        double sx;
+        HPDI_CNT(1);
+        const double gx = gfun<true>(P, xr, sx) - t;
+        if (fabs(gx) < 1e-12) break;
+        if ((gx < 0.0) == rising) rlo = xr;
+        else rhi = xr;
+        double xn = sx != 0.0 ? xr - gx / sx : 0.5 * (rlo + rhi);
+        if (!(rlo < xn && xn < rhi)) xn = 0.5 * (rlo + rhi);
+        const bool conv = fabs(xn - xr) < 0.05;
+        xr = xn;
+        if (conv) break;
+      }
+      xe[e] = xr;
     }
-    if (one >= 0) {
-      const double fx = pe[0];
-      const double F = log(M / (1.0 - M)) - log(kMass / (1.0 - kMass));
-      const double jac = one == 0 ? x + P.a : N - x + P.b;
-      const double dF = fx * jac * (1.0 / M + 1.0 / (1.0 - M));
-      double xn;
-      if (one == 0) {
-        if (F > 0.0) hb = x;
-        else lb = x;
-        xn = exp(log(x + P.a) - F / dF) - P.a;
-      } else {
-        if (F > 0.0) lb = x;
-        else hb = x;
-        xn = N + P.b - exp(log(N - x + P.b) - F / dF);
-      }
-      if (!(lb < xn && xn < hb)) xn = 0.5 * (lb + hb);
-      if (fabs(xn - x) < kStop || it >= 40) break;
-      x = xn;
-    } else {
-      if (M >= kMass) tL = t;
-      else tH = t;
-      double Dp = 0.0, mv = 0.0;
-      if (!cl) {
-        Dp += exp(t) / pe[0];
-        mv += 1.0 / pe[0];
-      }
-      if (!cr) {
-        Dp += exp(t) / -pe[1];
-        mv += 1.0 / -pe[1];
-      }
-      Dp *= P.pm;
-      if (it >= 40) break;
-      double tn;
-      if (Dp > 0.0) {
-        const double dt = (log(M) - log(kMass)) * M / Dp;
-        if (fabs(dt) * mv < kStop) break;
-        tn = t + dt;
-      } else {
-        tn = 0.5 * (tL + tH);  // both ends clamped: raise the level
-      }
-      if (!(tL < tn && tn < tH)) tn = tL > -INFINITY ? 0.5 * (tL + tH) : t - fmax(1.0, fabs(t));
-      t = tn;
-    }
+    W.xe0 = xe[0];
+    W.xe1 = xe[1];
+    A = ceil(xe[0]);
+    B = floor(xe[1]);
+  } else {
+    A = one == 0 ? 0.0 : ceil(W.x);
+    B = one == 0 ? floor(W.x) : N;
   }
-  // the fix-up from the end pmfs (one site for both)
+  const double M = wide_mass(P, A, B, W.sd) * P.pm;
+  W.A = A;
+  W.B = B;
+  W.M = M;
+  // the evaluations after the mass: f(x) (one-sided) or s at the two ends
+  double pe[2] = {0.0, 0.0};
+#pragma unroll 1
+  for (int e = 0; e < 2; ++e) {
+    const bool need = one >= 0 ? e == 0 : (e == 0 ? !cl : !cr);
+    if (!need) continue;
+    double sx;
+    HPDI_CNT(4);
+    const double gx = gfun<true>(P, one >= 0 ? W.x : xe[e], sx);
+    pe[e] = one >= 0 ? fexp(gx) * P.pm : sx;
+  }
+  W.it = it + 1;
+  if (one >= 0) {
+    const double x = W.x;
+    const double fx = pe[0];
+    const double F = log(M / (1.0 - M)) - log(kMass / (1.0 - kMass));
+    const double jac = one == 0 ? x + P.a : N - x + P.b;
+    const double dF = fx * jac * (1.0 / M + 1.0 / (1.0 - M));
+    double xn;
+    if (one == 0) {
+      if (F > 0.0) W.hb = x;
+      else W.lb = x;
+      xn = exp(log(x + P.a) - F / dF) - P.a;
+    } else {
+      if (F > 0.0) W.lb = x;
+      else W.hb = x;
+      xn = N + P.b - exp(log(N - x + P.b) - F / dF);
+    }
+    if (!(W.lb < xn && xn < W.hb)) xn = 0.5 * (W.lb + W.hb);
+    if (fabs(xn - x) < kStop || it >= 40) return true;
+    W.x = xn;
+    return false;
+  }
+  if (M >= kMass) W.tL = t;
+  else W.tH = t;
+  double Dp = 0.0, mv = 0.0;
+  if (!cl) {
+    Dp += exp(t) / pe[0];
+    mv += 1.0 / pe[0];
+  }
+  if (!cr) {
+    Dp += exp(t) / -pe[1];
+    mv += 1.0 / -pe[1];
+  }
+  Dp *= P.pm;
+  if (it >= 40) return true;
+  double tn;
+  if (Dp > 0.0) {
+    const double dt = (log(M) - log(kMass)) * M / Dp;
+    if (fabs(dt) * mv < kStop) return true;
+    tn = t + dt;
+  } else {
+    tn = 0.5 * (W.tL + W.tH);  // both ends clamped: raise the level
+  }
+  if (!(W.tL < tn && tn < W.tH)) tn = W.tL > -INFINITY ? 0.5 * (W.tL + W.tH) : t - fmax(1.0, fabs(t));
+  W.t = tn;
+  return false;
+}
+
+// the fix-up from the end pmfs (one site for both)
+__device__ __forceinline__ void wide_finish(const Wide& W, double& lo, double& hi) {
   double pAB[2];
 #pragma unroll 1
   for (int e = 0; e < 2; ++e) {
-    const bool need = e == 0 || B != A;
+    const bool need = e == 0 || W.B != W.A;
     if (need) HPDI_CNT(5);
-    pAB[e] = need ? fexp(g_of(P, e == 0 ? A : B)) * P.pm : pAB[0];
+    pAB[e] = need ? fexp(g_of(W.P, e == 0 ? W.A : W.B)) * W.P.pm : pAB[0];
   }
-  wide_fixup(P, A, B, M, pAB[0], pAB[1], lo, hi);
+  wide_fixup(W.P, W.A, W.B, W.M, pAB[0], pAB[1], lo, hi);
 }
 
 }  // namespace hpdi
