@@ -787,8 +787,11 @@ __global__ __launch_bounds__(kWave) void hpdi_prep_kernel(HpdiIO io, int64_t n_i
 // wave's evaluation sites stay busy whatever each window's iteration count.
 // Exit: a lane that draws an index past the list stops claiming; the wave
 // leaves when none of its lanes holds a window.
+#ifndef MDFIT_HPDI_WAVES_PER_EU
+#define MDFIT_HPDI_WAVES_PER_EU 2
+#endif
 template <bool kFit>
-__global__ __launch_bounds__(kWave) void hpdi_wide_kernel(HpdiIO io, int* __restrict__ ctr,
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPDI_WAVES_PER_EU))) void hpdi_wide_kernel(HpdiIO io, int* __restrict__ ctr,
                                                           const hpdi::WideRec* __restrict__ recs) {
   const int n_wide = ctr[0];  // written by K4a (stream-ordered)
   hpdi::Wide W;
