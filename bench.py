@@ -341,9 +341,14 @@ def nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, 
 
     S, W = 1000, 500
     k_avg_s = fit_ms_sum / n_calls / 1e3
-    # chain kernel: y,N in; 6 x S draws of 4 doubles + 6 x 4 diagnostics out
-    bytes_per_taxon = 240 + 6 * S * 32 + 6 * 32
+    # algorithmic bytes per SURVEY.md 8(d): y,N in + 26 result fields + the
+    # predictions (30 x 3 float32) out = 808 B/taxon; what the chain kernel moves
+    # as built -- y,N in, 6 x S draws of 4 doubles + 6 x 4 diagnostics out, the
+    # hand-off to the post kernel -- is the hbm_intermediate figure
+    bytes_per_taxon = ALG_BYTES_PER_TAXON + 30 * 3 * 4
+    draws_per_taxon = 240 + 6 * S * 32 + 6 * 32
     achieved = bytes_per_taxon * T / k_avg_s / 1e9
+    achieved_draws = draws_per_taxon * T / k_avg_s / 1e9
     leap = o[:, _lib.F_DIAG + 5 :: _lib.DIAG_STRIDE][:, :6]  # mean leapfrogs per kept iteration
     point_evals = float((leap * NPTS).sum() * (W + S))  # (warmup iterations counted at the kept rate)
     line = {
@@ -375,10 +380,17 @@ def nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, 
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": pmc_traffic("nuts_chain_kernel", T),
             "kernel": "nuts_chain_kernel",
-            "note": "HBM fraction is structural (the draws written, 192 KB per taxon, against ~2e6 leapfrog "
-            "point evaluations); the kernel is FP64-VALU / latency bound (DESIGN.md 9)",
+            "note": "algorithmic bytes per SURVEY.md 8(d) (y,N in + 26 result fields + 90 prediction values out "
+            "= 808 B/taxon); the HBM fraction is structural (~2e6 leapfrog point evaluations per taxon): the kernel "
+            "is FP64-VALU bound (DESIGN.md 9); traffic is the PMC-measured HBM bytes, dominated by the draws",
             "kernel_ms_avg": round(k_avg_s * 1e3, 3),
             "bytes_per_taxon": bytes_per_taxon,
+            "hbm_intermediate": {
+                "bytes_per_taxon": draws_per_taxon,
+                "achieved": round(achieved_draws, 3),
+                "note": "what the chain kernel moves as built: y,N in, the 6 x 1000 draws (q, A, c, phi) and "
+                "diagnostics out -- the hand-off to nuts_post_kernel",
+            },
             "call_ms_avg": round(call_ms_sum / n_calls, 3),
         },
         "leapfrog_point_evals_per_s": round(point_evals / k_avg_s, 1),

@@ -55,19 +55,19 @@ def main() -> None:
     for name in ("bench_trace.json", "bench_nuts_trace.json"):
         if (src / name).exists():
             shutil.copy(src / name, prof / f"{tag}_{name}")
-    write_summary(prof, tag, "fit_kernel", TAXA, FIT_BYTES_PER_TAXON, found["kernel_stats.csv"],
+    write_summary(prof, tag, "fit_kernel", TAXA, FIT_BYTES_PER_TAXON, 448, found["kernel_stats.csv"],
                   found["pmc_fetch_size.csv"], found["pmc_write_size.csv"], "python bench.py")
     # the NUTS chain kernel at config C3 (optional passes)
     nf, nw = sorted((src / "nuts_fetch").rglob("*counter_collection.csv")), sorted((src / "nuts_write").rglob("*counter_collection.csv"))
     if nuts and nf and nw:
         shutil.copy(nf[0], prof / f"{tag}_nuts_pmc_fetch_size.csv")
         shutil.copy(nw[0], prof / f"{tag}_nuts_pmc_write_size.csv")
-        write_summary(prof, tag, "nuts_chain_kernel", NUTS_TAXA, NUTS_BYTES_PER_TAXON,
+        write_summary(prof, tag, "nuts_chain_kernel", NUTS_TAXA, NUTS_BYTES_PER_TAXON, 808,
                       prof / f"{tag}_nuts_kernel_stats.csv", prof / f"{tag}_nuts_pmc_fetch_size.csv",
                       prof / f"{tag}_nuts_pmc_write_size.csv", "python bench.py --mode nuts")
 
 
-def write_summary(prof, tag, name, taxa, bytes_per_taxon, stats_csv, fetch_csv, write_csv, cmd):
+def write_summary(prof, tag, name, taxa, bytes_per_taxon, alg_per_taxon, stats_csv, fetch_csv, write_csv, cmd):
     k = f"mdfit::{name}" if name == "fit_kernel" else f"mdfit::nuts::{name}"
     fetch_kb = counter_mean(fetch_csv, k, "FETCH_SIZE")
     write_kb = counter_mean(write_csv, k, "WRITE_SIZE")
@@ -81,7 +81,11 @@ def write_summary(prof, tag, name, taxa, bytes_per_taxon, stats_csv, fetch_csv, 
         "correction": "gfx950: FETCH_SIZE x2 (MI355X_MICROARCH.md §HBM: FETCH_SIZE reports 1/2 of wide coalesced "
         "reads; this kernel's 4-B/lane and broadcast 8-B loads are uncalibrated), WRITE_SIZE x1",
         "hbm_bytes_per_launch": int(round((2 * fetch_kb + write_kb) * 1024)),
-        "algorithmic_bytes_per_launch": bytes_per_taxon * taxa,
+        "handoff_bytes_per_launch": bytes_per_taxon * taxa,
+        "handoff_note": "what the kernel moves as built (the hand-off to the next kernel: MAP the 6 sub-fit records, "
+        "NUTS the draws)",
+        "survey_algorithmic_bytes_per_launch": alg_per_taxon * taxa,
+        "survey_note": "SURVEY.md 8(d): y,N in + 26 result fields out (+ 90 prediction values for NUTS)",
         "rocprof_avg_ns": float(fk.get("AverageNs", "nan")),
         "source": f"rocprofv3 --kernel-trace --stats; --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes; "
         f"{cmd} (profiles/{tag}_*.csv)",
