@@ -72,6 +72,8 @@ def parse():
     ap.add_argument("--mode", choices=["map", "nuts"], default="map",
                     help="map: config C2 (the headline); nuts: config C3, the reference's sampler")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c4-base", action="store_true",
+                    help="N=1: skip the C4-on-one-GPU strong-scaling base (c4_one_gpu)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the process's core share (affinity, OMP_NUM_THREADS)")
     ap.add_argument("--workload", choices=["c2", "c4"], default=None,
                     help="default: c2 at N = 1 (the headline), c4 (1M taxa, strong scaling) at N > 1")
@@ -95,6 +97,45 @@ def pmc_traffic(kernel: str = "fit_kernel", taxa: int = TAXA_PER_GPU):
         return d.get("hbm_bytes_per_launch") if d.get("taxa_per_launch") == taxa else None
     except Exception:
         return None
+
+
+def c4_one_gpu(engine, _lib, generate, dev, stream, steps: int = 3, warmup: int = 1) -> dict:
+    """The strong-scaling base of the N>1 lines: C4's 1M TaxIDs fitted on ONE GPU
+    in one call, inputs resident in HBM.  1M synthetic taxa take ~1 min to
+    generate on the host, so C4's rank-0 share (125k, seed 3) is tiled 8x on
+    the device -- the same per-taxon work distribution."""
+    import torch
+
+    share, reps = C4_TAXA // 8, 8
+    b = generate(share, seed=3)
+    ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm, device=dev)
+    ty, tN, tm = (x.repeat((reps,) + (1,) * (x.dim() - 1)).contiguous() for x in (ty, tN, tm))
+    T = share * reps
+    opts = _lib.default_opts(mode=_lib.MODE_MAP)
+    fb = engine.alloc_outputs(T, device=dev, opts=opts)
+    for _ in range(warmup):
+        engine.fit_batch_device(ty, tN, tm, opts, fb, stream=stream)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        engine.fit_batch_device(ty, tN, tm, opts, fb, stream=stream)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    ok = float((fb.status == 0).float().mean().item())
+    del ty, tN, tm, fb
+    torch.cuda.empty_cache()
+    return {
+        "value": round(T * steps / el, 1),
+        "unit": "fits/s",
+        "ms_per_step": round(el / steps * 1e3, 3),
+        "taxa": T,
+        "steps": steps,
+        "warmup": warmup,
+        "status_ok_frac": ok,
+        "data": f"C4's rank-0 share ({share} synthetic TaxIDs, seed 3) tiled {reps}x on the device",
+        "note": "the strong-scaling base for the N>1 lines (C4: 1M TaxIDs, 1M/N per rank + one gather): "
+        "efficiency_N = value_N / (N * this value)",
+    }
 
 
 def host_cores() -> tuple[int, int]:
@@ -291,6 +332,8 @@ def main():
         }
         if world == 1:
             line["host_to_host"] = host_to_host(engine, b, opts, dev, max(5, args.steps // 2))
+        if world == 1 and workload == "c2" and not args.no_c4_base:
+            line["c4_one_gpu"] = c4_one_gpu(engine, _lib, generate, dev, stream)
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure
             line["cpu_baseline"], ref = cpu_baseline(b, cores, visible)
             if ref_dispatch is not None:
