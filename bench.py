@@ -187,10 +187,20 @@ def main():
     from metadamage_amd.distributed import alloc_records, gather_records, shard_capacity, shard_range
     from metadamage_amd.synthetic import generate
 
+    # development rehearsal of the N>1 path on a one-GPU box: every rank on
+    # cuda:0, gloo instead of RCCL (the gather stages through the host); the
+    # measured lines use one GPU per rank and RCCL
+    share_gpu = os.environ.get("MDFIT_BENCH_SHARE_GPU") == "1"
+    if share_gpu:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if share_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    red_dev = torch.device("cpu") if share_gpu else dev
 
     # ---- synthetic shard, resident in HBM before timing -------------------
     if workload == "c4":
@@ -229,7 +239,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     _, fit_ms_sum, n_calls = engine.profile_read()
