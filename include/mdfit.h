@@ -130,8 +130,12 @@ void mdfit_default_opts(mdfit_opts* opts);
  *   out       : double[n_taxa][MDFIT_NOUT]                  (device)
  *   pred      : float[n_taxa][MDFIT_NPRED][MDFIT_NPOS] or NULL (device)
  *   status    : int32_t[n_taxa]                             (device)
- *   workspace : device buffer of mdfit_workspace_bytes(n_taxa) bytes (work queues)
- *   hip_stream: hipStream_t or NULL
+ *   workspace : device buffer of mdfit_workspace_bytes(n_taxa) bytes (work
+ *               queues, the PMD-all mode for the HPDI, the wide-window list)
+ *   hip_stream: hipStream_t or NULL.  MAP: the record assembly runs on a
+ *               library-owned side stream (one per host thread and device),
+ *               forked from and joined back into hip_stream by events, so the
+ *               call stays ordered on hip_stream and capturable in a graph
  * Replaces compute_fits' per-taxon loop (fits.py:477-526, 569-626, 709-730).
  */
 int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm,

@@ -687,8 +687,35 @@ __global__ __launch_bounds__(kWave) void assemble_kernel(
   record_sums_noise(lane, s_y, s_N, s_mm, gmm != nullptr, s_rec, s_tmp);
 
   __syncthreads();
-  for (int i = lane; i < MDFIT_NOUT; i += kWave) out[t * MDFIT_NOUT + i] = s_rec[i];
+  // every field but the two HPDI columns, which K4 writes (it runs beside this
+  // kernel on the caller's stream)
+  for (int i = lane; i < MDFIT_NOUT; i += kWave)
+    if (i != MDFIT_F_D_MAX_LOWER_HPDI && i != MDFIT_F_D_MAX_UPPER_HPDI) out[t * MDFIT_NOUT + i] = s_rec[i];
   if (lane == 0) status[t] = st;
+}
+
+// K3a: the PMD-all mode u* -> (q, A, c, phi) into the workspace for K4 (the
+// same arithmetic as make_theta, so K4 sees the values K3 writes to the
+// record); NaN for a taxon with invalid input (y > N somewhere: K3 writes a NaN
+// record for it, K4 then NaN windows).  One thread per taxon.
+__global__ __launch_bounds__(256) void theta_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN,
+                                                    int64_t n_taxa, const double* __restrict__ out,
+                                                    double* __restrict__ theta) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_taxa) return;
+  bool bad = false;
+  for (int i = 0; i < kNPos; ++i) bad = bad || gy[t * kLD + i] > gN[t * kLD + i];
+  const double* dg = out + t * MDFIT_NOUT + MDFIT_F_DIAG;  // sub-fit 0: u*
+  auto sig = [](double v) {
+    const double e = exp(-fabs(v));
+    const double rr = rcp(1.0 + e);
+    return v >= 0.0 ? rr : e * rr;
+  };
+  const double q = sig(dg[0]), A = sig(dg[1]), c = dg[2], phi = exp(dg[3]) + 2.0;
+  theta[t * 4 + 0] = bad ? NAN : q;
+  theta[t * 4 + 1] = bad ? NAN : A;
+  theta[t * 4 + 2] = bad ? NAN : c;
+  theta[t * 4 + 3] = bad ? NAN : phi;
 }
 
 // ---------------------------------------------------------------------------
@@ -707,6 +734,7 @@ constexpr int kHpdiCtr = 16;  // workspace ints: [16] wide count, [17] claim cou
 struct HpdiIO {
   // kFit
   const uint32_t* gN;
+  const double* theta;  // PMD-all (q, A, c, phi) per taxon (K3a)
   double* out;
   float* pred;
   int per;  // positions per taxon written (30, or 1 without pred)
@@ -746,7 +774,7 @@ __global__ __launch_bounds__(kWave) void hpdi_prep_kernel(HpdiIO io, int64_t n_i
     if (kFit) {
       const int64_t t = item / io.per;
       const int i = (int)(item - t * io.per);
-      const double* dg = io.out + t * MDFIT_NOUT + MDFIT_F_DIAG;  // PMD-all: (q, A, c, phi)
+      const double* dg = io.theta + t * 4;  // PMD-all: (q, A, c, phi)
       const double q = dg[0], A = dg[1], c = dg[2], phi = dg[3];
       N = (double)io.gN[t * kLD + i];
       if (N > 0.0 && !isnan(q)) {
@@ -993,9 +1021,25 @@ void prof_record(int slot, hipStream_t s) {
 }  // namespace
 
 namespace {
-// HPDI wide-window records follow the 256 B of counters in the MAP workspace
-mdfit::hpdi::WideRec* hpdi_recs(void* ws) {
-  return reinterpret_cast<mdfit::hpdi::WideRec*>(static_cast<char*>(ws) + 256);
+// MAP workspace: 256 B of counters, the PMD-all (q, A, c, phi) of every taxon
+// (K3a -> K4; n_theta = n_taxa, 0 for the array entry point), then the HPDI
+// wide-window records
+double* theta_buf(void* ws) { return reinterpret_cast<double*>(static_cast<char*>(ws) + 256); }
+mdfit::hpdi::WideRec* hpdi_recs(void* ws, int64_t n_theta) {
+  return reinterpret_cast<mdfit::hpdi::WideRec*>(static_cast<char*>(ws) + 256 + n_theta * 4 * (int64_t)sizeof(double));
+}
+
+// The side stream of mdfit_fit_batch's fork (the record assembly runs there
+// beside the HPDI kernels): one per host thread and device, created on first
+// use, non-blocking (ordered against the caller's stream by events only).
+hipStream_t side_stream() {
+  constexpr int kMaxDev = 64;
+  static thread_local hipStream_t side[kMaxDev] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
+  if (side[dev] == nullptr && hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking) != hipSuccess)
+    side[dev] = nullptr;
+  return side[dev];
 }
 
 template <bool kFit>
@@ -1069,7 +1113,7 @@ int64_t mdfit_workspace_bytes(int64_t n_taxa, const mdfit_opts* opts) {
   if (o.mode == MDFIT_MODE_NUTS) return mdfit::nuts::workspace_bytes(n_taxa, o.num_samples);
   // the 8 per-XCD queue counters + the HPDI list counters (int32, 256 B), then
   // room for every position's wide-window record (MDFIT-HPDI v1)
-  return 256 + n_taxa * mdfit::kNPos * (int64_t)sizeof(mdfit::hpdi::WideRec);
+  return 256 + n_taxa * 4 * (int64_t)sizeof(double) + n_taxa * mdfit::kNPos * (int64_t)sizeof(mdfit::hpdi::WideRec);
 }
 
 int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t n_taxa,
@@ -1116,17 +1160,38 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   }
   if (int rc = check_launch("fit_kernel")) return rc;
   prof_record(2, s);
-  hipLaunchKernelGGL(mdfit::assemble_kernel, dim3((unsigned)n_taxa), dim3(mdfit::kWave), 0, s, y, N,
+  // K3a (the PMD-all mode for K4), then a fork: the record assembly (K3) on
+  // the side stream, the predictive HPDI (K4a, K4b) on the caller's; they
+  // write disjoint fields of the record and join before the call returns
+  double* theta = theta_buf(workspace);
+  hipLaunchKernelGGL(mdfit::theta_kernel, dim3((unsigned)((n_taxa + 255) / 256)), dim3(256), 0, s, y, N, n_taxa,
+                     out, theta);
+  if (int rc = check_launch("theta_kernel")) return rc;
+  hipStream_t s2 = side_stream();
+  hipEvent_t e_fork = nullptr, e_join = nullptr;
+  const bool fork = s2 != nullptr && hipEventCreateWithFlags(&e_fork, hipEventDisableTiming) == hipSuccess &&
+                    hipEventCreateWithFlags(&e_join, hipEventDisableTiming) == hipSuccess &&
+                    hipEventRecord(e_fork, s) == hipSuccess && hipStreamWaitEvent(s2, e_fork, 0) == hipSuccess;
+  hipStream_t sa = fork ? s2 : s;  // no side stream: everything in order on s
+  hipLaunchKernelGGL(mdfit::assemble_kernel, dim3((unsigned)n_taxa), dim3(mdfit::kWave), 0, sa, y, N,
                      mm, n_taxa, out, pred, status);
   if (int rc = check_launch("assemble_kernel")) return rc;
   {
     mdfit::HpdiIO io{};
     io.gN = N;
+    io.theta = theta;
     io.out = out;
     io.pred = pred;
     io.per = pred != nullptr ? mdfit::kNPos : 1;
-    if (int rc = launch_hpdi<true>(io, n_taxa * io.per, ws + mdfit::kHpdiCtr, hpdi_recs(workspace), s)) return rc;
+    if (int rc = launch_hpdi<true>(io, n_taxa * io.per, ws + mdfit::kHpdiCtr, hpdi_recs(workspace, n_taxa), s))
+      return rc;
   }
+  if (fork) {
+    if (hipEventRecord(e_join, s2) != hipSuccess || hipStreamWaitEvent(s, e_join, 0) != hipSuccess)
+      return set_err(MDFIT_E_HIP, "stream join");
+  }
+  if (e_fork) (void)hipEventDestroy(e_fork);  // released once complete
+  if (e_join) (void)hipEventDestroy(e_join);
   prof_record(3, s);
   if (g_prof.on && g_prof.n < kProfMax) ++g_prof.n;
   return 0;
@@ -1168,7 +1233,7 @@ int mdfit_hpdi68(const double* N, const double* alpha, const double* beta, int64
   io.b = beta;
   io.lo = lo;
   io.hi = hi;
-  int rc = launch_hpdi<false>(io, n, static_cast<int*>(ws) + mdfit::kHpdiCtr, hpdi_recs(ws), s);
+  int rc = launch_hpdi<false>(io, n, static_cast<int*>(ws) + mdfit::kHpdiCtr, hpdi_recs(ws, 0), s);
   (void)hipFreeAsync(ws, s);
   return rc;
 }
