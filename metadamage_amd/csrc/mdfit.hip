@@ -729,7 +729,7 @@ __global__ __launch_bounds__(256) void theta_kernel(const uint32_t* __restrict__
 // -> only z = +1, the D_max_{lower,upper}_hpdi columns) or plain arrays
 // (mdfit_hpdi68, parity tests).
 // ---------------------------------------------------------------------------
-constexpr int kHpdiCtr = 16;  // workspace ints: [16] wide count, [17] claim counter (zeroed by K0)
+constexpr int kHpdiCtr = 16;  // workspace ints: [16] front-list count, [17] claim counter, [18] back-list count (zeroed by K0)
 
 struct HpdiIO {
   // kFit
@@ -798,14 +798,30 @@ __global__ __launch_bounds__(kWave) void hpdi_prep_kernel(HpdiIO io, int64_t n_i
     if (!skip) wide = !hpdi::prep_position(N, a, b, lo, hi, rec);
     if (!wide) hpdi_write<kFit>(io, item, N, lo, hi);
   }
-  const unsigned long long m = __ballot(wide);
-  if (m == 0ull) return;
-  int base = 0;
-  if (threadIdx.x == 0) base = atomicAdd(ctr, __popcll(m));
-  base = __shfl(base, 0);
+  // two lists in one buffer of n_items records, drained longest-first by K4b:
+  // windows whose mode lies within 1.5 tau of a support end (log-variable
+  // panels, support-end walks, one-sided windows: ~2.5 level iterations) from
+  // the front (count ctr[0]), the clean two-sided ones (~1.45) from the back
+  // (count ctr[2])
+  bool near = false;
+  if (wide) {
+    const double tau = sqrt(rec.sd * rec.sd + (rec.mu - rec.m) * (rec.mu - rec.m));
+    near = rec.m < 1.5 * tau || rec.N - rec.m < 1.5 * tau;
+  }
+  const unsigned long long mf = __ballot(wide && near), mb = __ballot(wide && !near);
+  if ((mf | mb) == 0ull) return;
+  int bf = 0, bb = 0;
+  if (threadIdx.x == 0) {
+    if (mf) bf = atomicAdd(ctr, __popcll(mf));
+    if (mb) bb = atomicAdd(ctr + 2, __popcll(mb));
+  }
+  bf = __shfl(bf, 0);
+  bb = __shfl(bb, 0);
   if (wide) {
     rec.item = item;
-    recs[base + __popcll(m & ((1ull << threadIdx.x) - 1ull))] = rec;
+    const unsigned long long below = (1ull << threadIdx.x) - 1ull;
+    const int64_t slot = near ? (int64_t)(bf + __popcll(mf & below)) : n_items - 1 - (bb + __popcll(mb & below));
+    recs[slot] = rec;
   }
 }
 
@@ -819,9 +835,9 @@ __global__ __launch_bounds__(kWave) void hpdi_prep_kernel(HpdiIO io, int64_t n_i
 #define MDFIT_HPDI_WAVES_PER_EU 2
 #endif
 template <bool kFit>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPDI_WAVES_PER_EU))) void hpdi_wide_kernel(HpdiIO io, int* __restrict__ ctr,
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPDI_WAVES_PER_EU))) void hpdi_wide_kernel(HpdiIO io, int64_t n_items, int* __restrict__ ctr,
                                                           const hpdi::WideRec* __restrict__ recs) {
-  const int n_wide = ctr[0];  // written by K4a (stream-ordered)
+  const int n_front = ctr[0], n_wide = n_front + ctr[2];  // written by K4a (stream-ordered)
   hpdi::Wide W;
   int64_t item = 0;
   bool busy = false, drained = false;
@@ -835,7 +851,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
       if (need) {
         const int idx = base + __popcll(m & ((1ull << threadIdx.x) - 1ull));
         if (idx < n_wide) {
-          const hpdi::WideRec r = recs[idx];
+          const hpdi::WideRec r = recs[idx < n_front ? (int64_t)idx : n_items - 1 - (idx - n_front)];
           item = r.item;
           hpdi::wide_start(W, r);
           busy = true;
@@ -1051,7 +1067,8 @@ int launch_hpdi(const mdfit::HpdiIO& io, int64_t n_items, int* ctr, mdfit::hpdi:
   // no more waves than are resident, and no more than the items need (the
   // kernel strides over the wide list, whose length only the device knows)
   const int64_t g = fit_grid(mdfit::hpdi_wide_kernel<kFit>, n_items, mdfit::kWave);
-  hipLaunchKernelGGL(mdfit::hpdi_wide_kernel<kFit>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, io, ctr, recs);
+  hipLaunchKernelGGL(mdfit::hpdi_wide_kernel<kFit>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, io, n_items, ctr,
+                     recs);
   return check_launch("hpdi_wide_kernel");
 }
 }  // namespace
