@@ -162,10 +162,89 @@ constexpr int kPrioEvals = 15;  // fit length (evaluations) that raises the wave
 constexpr unsigned kEscIndef = 1u, kEscProbe = 2u, kEscNc = 4u, kEscExhOk = 8u, kEscN = 16u, kEscCount = 0x70u,
                    kEscRescued = 0x100u, kEscRelax = 0x200u;
 
+// ---------------------------------------------------------------------------
+// The predictive HPDI's per-position step (K4a, and the fused prep of the PPL-1
+// fit kernel): shared definitions
+// ---------------------------------------------------------------------------
+constexpr int kHpdiCtr = 16;  // workspace ints: [16] front-list count, [17] claim counter, [18] back-list count (zeroed by K0)
+
+struct HpdiIO {
+  // kFit
+  const uint32_t* gN;
+  const double* theta;  // PMD-all (q, A, c, phi) per taxon (K3a)
+  double* out;
+  float* pred;
+  int per;  // positions per taxon written (30, or 1 without pred)
+  // arrays
+  const double *N, *a, *b;
+  double *lo, *hi;
+};
+
+template <bool kFit>
+__device__ __forceinline__ void hpdi_write(const HpdiIO& io, int64_t item, double N, double lo, double hi) {
+  if (kFit) {
+    const int64_t t = item / io.per;
+    const int i = (int)(item - t * io.per);
+    const double fl = N > 0.0 ? lo / N : NAN, fh = N > 0.0 ? hi / N : NAN;
+    if (io.pred != nullptr) {
+      io.pred[t * (MDFIT_NPRED * kNPos) + 1 * kNPos + i] = (float)fl;
+      io.pred[t * (MDFIT_NPRED * kNPos) + 2 * kNPos + i] = (float)fh;
+    }
+    if (i == 0) {
+      io.out[t * MDFIT_NOUT + MDFIT_F_D_MAX_LOWER_HPDI] = fl;
+      io.out[t * MDFIT_NOUT + MDFIT_F_D_MAX_UPPER_HPDI] = fh;
+    }
+  } else {
+    io.lo[item] = lo;
+    io.hi[item] = hi;
+  }
+}
+
+// the position's window (greedy, written here) or its wide record, appended to
+// the two-list buffer that K4b drains longest-first: windows whose mode lies
+// within 1.5 tau of a support end (log-variable panels, support-end walks,
+// one-sided windows: ~2.5 level iterations) from the front (count ctr[0]), the
+// clean two-sided ones (~1.45) from the back (count ctr[2]).  Wave-collective
+// over the active lanes (the first one does the list atomics).
+template <bool kFit>
+__device__ __forceinline__ void hpdi_position(const HpdiIO& io, int64_t item, bool valid, bool skip, double N, double a,
+                                              double b, int64_t n_items, int* __restrict__ ctr,
+                                              hpdi::WideRec* __restrict__ recs) {
+  bool wide = false;
+  hpdi::WideRec rec;
+  if (valid) {
+    double lo = NAN, hi = NAN;
+    if (!skip) wide = !hpdi::prep_position(N, a, b, lo, hi, rec);
+    if (!wide) hpdi_write<kFit>(io, item, N, lo, hi);
+  }
+  bool near = false;
+  if (wide) {
+    const double tau = sqrt(rec.sd * rec.sd + (rec.mu - rec.m) * (rec.mu - rec.m));
+    near = rec.m < 1.5 * tau || rec.N - rec.m < 1.5 * tau;
+  }
+  const int first = __ffsll((unsigned long long)__ballot(1)) - 1;
+  const unsigned long long mf = __ballot(wide && near), mb = __ballot(wide && !near);
+  if ((mf | mb) == 0ull) return;
+  int bf = 0, bb = 0;
+  if ((int)threadIdx.x == first) {
+    if (mf) bf = atomicAdd(ctr, __popcll(mf));
+    if (mb) bb = atomicAdd(ctr + 2, __popcll(mb));
+  }
+  bf = __shfl(bf, first);
+  bb = __shfl(bb, first);
+  if (wide) {
+    rec.item = item;
+    const unsigned long long below = (1ull << threadIdx.x) - 1ull;
+    const int64_t slot = near ? (int64_t)(bf + __popcll(mf & below)) : n_items - 1 - (bb + __popcll(mb & below));
+    recs[slot] = rec;
+  }
+}
+
 template <int PPL>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_FIT_WAVES_PER_EU)))
 void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN, int64_t T,
-                int max_iter, double tol, double* __restrict__ out, int* __restrict__ ws) {
+                int max_iter, double tol, double* __restrict__ out, int* __restrict__ ws, float* __restrict__ pred,
+                int per, int* __restrict__ hctr, hpdi::WideRec* __restrict__ hrecs) {
   static_assert(PPL == 1 || PPL == 2, "points per lane");
   constexpr int kSlot = PPL == 1 ? 32 : 16;  // lanes per slot (one all-position fit or one pair)
   constexpr int kHalf = kSlot / 2;           // lanes per fwd/rev sub-fit of a pair
@@ -493,8 +572,40 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
     // continues with its pair, a pair with the next task
     const unsigned long long busy = __ballot(running);
     if ((busy & slot_mask) == 0ull) {
-      if (mode == kAllFit) mode = kNextPair;
-      else if (mode == kPairFit) mode = kIdle;
+      if (mode == kAllFit) {
+        if (PPL == 1 && sub == 0 && hrecs != nullptr) {
+          // the PMD-all fit just ended: the predictive HPDI's per-position step
+          // here (K4a's work, lane = position; the same arithmetic as
+          // theta_kernel + hpdi_prep_kernel), its wide windows to K4b's list
+          HpdiIO io{};
+          io.gN = gN;
+          io.out = out;
+          io.pred = pred;
+          io.per = per;
+          auto sig = [](double v) {
+            const double e = exp(-fabs(v));
+            const double rr = rcp(1.0 + e);
+            return v >= 0.0 ? rr : e * rr;
+          };
+          const double q = sig(u[0]), A = sig(u[1]), c = u[2], phi = exp(u[3]) + 2.0;
+          const bool bad = (__ballot(vA_all && pa.y > pa.N) & slot_mask) != 0ull;  // invalid input: NaN windows
+          const bool valid = vA_all && (per == kNPos || colA_all == 0);
+          const int64_t item = per == kNPos ? taxon * kNPos + colA_all : taxon;
+          const double N = pa.N;
+          double a = 0.0, b = 0.0;
+          bool skip = true;
+          if (valid && N > 0.0 && !bad && !isnan(q)) {
+            const double D = fmin(fma(A, powk(1.0 - q, kA_all), c), 1.0);
+            a = D * phi;
+            b = (1.0 - D) * phi;
+            skip = false;
+          }
+          hpdi_position<true>(io, item, valid, skip, N, a, b, T * per, hctr, hrecs);
+        }
+        mode = kNextPair;
+      } else if (mode == kPairFit) {
+        mode = kIdle;
+      }
     }
 #ifdef MDFIT_STAMP
     const unsigned long long l1 = stamp();
@@ -729,40 +840,6 @@ __global__ __launch_bounds__(256) void theta_kernel(const uint32_t* __restrict__
 // -> only z = +1, the D_max_{lower,upper}_hpdi columns) or plain arrays
 // (mdfit_hpdi68, parity tests).
 // ---------------------------------------------------------------------------
-constexpr int kHpdiCtr = 16;  // workspace ints: [16] front-list count, [17] claim counter, [18] back-list count (zeroed by K0)
-
-struct HpdiIO {
-  // kFit
-  const uint32_t* gN;
-  const double* theta;  // PMD-all (q, A, c, phi) per taxon (K3a)
-  double* out;
-  float* pred;
-  int per;  // positions per taxon written (30, or 1 without pred)
-  // arrays
-  const double *N, *a, *b;
-  double *lo, *hi;
-};
-
-template <bool kFit>
-__device__ __forceinline__ void hpdi_write(const HpdiIO& io, int64_t item, double N, double lo, double hi) {
-  if (kFit) {
-    const int64_t t = item / io.per;
-    const int i = (int)(item - t * io.per);
-    const double fl = N > 0.0 ? lo / N : NAN, fh = N > 0.0 ? hi / N : NAN;
-    if (io.pred != nullptr) {
-      io.pred[t * (MDFIT_NPRED * kNPos) + 1 * kNPos + i] = (float)fl;
-      io.pred[t * (MDFIT_NPRED * kNPos) + 2 * kNPos + i] = (float)fh;
-    }
-    if (i == 0) {
-      io.out[t * MDFIT_NOUT + MDFIT_F_D_MAX_LOWER_HPDI] = fl;
-      io.out[t * MDFIT_NOUT + MDFIT_F_D_MAX_UPPER_HPDI] = fh;
-    }
-  } else {
-    io.lo[item] = lo;
-    io.hi[item] = hi;
-  }
-}
-
 template <bool kFit>
 __global__ __launch_bounds__(kWave) void hpdi_prep_kernel(HpdiIO io, int64_t n_items, int* __restrict__ ctr,
                                                           hpdi::WideRec* __restrict__ recs) {
@@ -791,38 +868,7 @@ __global__ __launch_bounds__(kWave) void hpdi_prep_kernel(HpdiIO io, int64_t n_i
       skip = !(N > 0.0);
     }
   }
-  bool wide = false;
-  hpdi::WideRec rec;
-  if (valid) {
-    double lo = NAN, hi = NAN;
-    if (!skip) wide = !hpdi::prep_position(N, a, b, lo, hi, rec);
-    if (!wide) hpdi_write<kFit>(io, item, N, lo, hi);
-  }
-  // two lists in one buffer of n_items records, drained longest-first by K4b:
-  // windows whose mode lies within 1.5 tau of a support end (log-variable
-  // panels, support-end walks, one-sided windows: ~2.5 level iterations) from
-  // the front (count ctr[0]), the clean two-sided ones (~1.45) from the back
-  // (count ctr[2])
-  bool near = false;
-  if (wide) {
-    const double tau = sqrt(rec.sd * rec.sd + (rec.mu - rec.m) * (rec.mu - rec.m));
-    near = rec.m < 1.5 * tau || rec.N - rec.m < 1.5 * tau;
-  }
-  const unsigned long long mf = __ballot(wide && near), mb = __ballot(wide && !near);
-  if ((mf | mb) == 0ull) return;
-  int bf = 0, bb = 0;
-  if (threadIdx.x == 0) {
-    if (mf) bf = atomicAdd(ctr, __popcll(mf));
-    if (mb) bb = atomicAdd(ctr + 2, __popcll(mb));
-  }
-  bf = __shfl(bf, 0);
-  bb = __shfl(bb, 0);
-  if (wide) {
-    rec.item = item;
-    const unsigned long long below = (1ull << threadIdx.x) - 1ull;
-    const int64_t slot = near ? (int64_t)(bf + __popcll(mf & below)) : n_items - 1 - (bb + __popcll(mb & below));
-    recs[slot] = rec;
-  }
+  hpdi_position<kFit>(io, item, valid, skip, N, a, b, n_items, ctr, recs);
 }
 
 // one lane per wide window at a time: every trip each busy lane runs one level
@@ -1058,12 +1104,16 @@ hipStream_t side_stream() {
   return side[dev];
 }
 
+// K4a (unless the fit kernel did its work: prep = false) and K4b
 template <bool kFit>
-int launch_hpdi(const mdfit::HpdiIO& io, int64_t n_items, int* ctr, mdfit::hpdi::WideRec* recs, hipStream_t s) {
+int launch_hpdi(const mdfit::HpdiIO& io, int64_t n_items, int* ctr, mdfit::hpdi::WideRec* recs, hipStream_t s,
+                bool prep = true) {
   if (n_items == 0) return 0;
-  hipLaunchKernelGGL(mdfit::hpdi_prep_kernel<kFit>, dim3((unsigned)((n_items + mdfit::kWave - 1) / mdfit::kWave)),
-                     dim3(mdfit::kWave), 0, s, io, n_items, ctr, recs);
-  if (int rc = check_launch("hpdi_prep_kernel")) return rc;
+  if (prep) {
+    hipLaunchKernelGGL(mdfit::hpdi_prep_kernel<kFit>, dim3((unsigned)((n_items + mdfit::kWave - 1) / mdfit::kWave)),
+                       dim3(mdfit::kWave), 0, s, io, n_items, ctr, recs);
+    if (int rc = check_launch("hpdi_prep_kernel")) return rc;
+  }
   // no more waves than are resident, and no more than the items need (the
   // kernel strides over the wide list, whose length only the device knows)
   const int64_t g = fit_grid(mdfit::hpdi_wide_kernel<kFit>, n_items, mdfit::kWave);
@@ -1166,24 +1216,30 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   int ppl = n_taxa >= kPpl2MinTaxa ? 2 : 1;
   if (const char* e = std::getenv("MDFIT_FIT_PPL")) ppl = std::atoi(e) == 2 ? 2 : 1;
   prof_record(1, s);
+  const int per = pred != nullptr ? mdfit::kNPos : 1;
+  mdfit::hpdi::WideRec* recs = hpdi_recs(workspace, n_taxa);
+  int* hctr = ws + mdfit::kHpdiCtr;
   if (ppl == 2) {
     const int64_t g = fit_grid(mdfit::fit_kernel<2>, 2 * n_taxa, 4);
     hipLaunchKernelGGL(mdfit::fit_kernel<2>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, y, N, n_taxa,
-                       o.max_iter, o.tol_step, out, ws);
+                       o.max_iter, o.tol_step, out, ws, pred, per, hctr, (mdfit::hpdi::WideRec*)nullptr);
   } else {
+    // PPL 1 also runs the HPDI's per-position step (K4a) as each PMD-all fit ends
     const int64_t g = fit_grid(mdfit::fit_kernel<1>, 2 * n_taxa, 2);
     hipLaunchKernelGGL(mdfit::fit_kernel<1>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, y, N, n_taxa,
-                       o.max_iter, o.tol_step, out, ws);
+                       o.max_iter, o.tol_step, out, ws, pred, per, hctr, recs);
   }
   if (int rc = check_launch("fit_kernel")) return rc;
   prof_record(2, s);
-  // K3a (the PMD-all mode for K4), then a fork: the record assembly (K3) on
-  // the side stream, the predictive HPDI (K4a, K4b) on the caller's; they
-  // write disjoint fields of the record and join before the call returns
+  // (PPL 2: K3a, the PMD-all mode for K4a), then a fork: the record assembly
+  // (K3) on the side stream, the predictive HPDI (K4a, K4b) on the caller's;
+  // they write disjoint fields of the record and join before the call returns
   double* theta = theta_buf(workspace);
-  hipLaunchKernelGGL(mdfit::theta_kernel, dim3((unsigned)((n_taxa + 255) / 256)), dim3(256), 0, s, y, N, n_taxa,
-                     out, theta);
-  if (int rc = check_launch("theta_kernel")) return rc;
+  if (ppl == 2) {
+    hipLaunchKernelGGL(mdfit::theta_kernel, dim3((unsigned)((n_taxa + 255) / 256)), dim3(256), 0, s, y, N, n_taxa,
+                       out, theta);
+    if (int rc = check_launch("theta_kernel")) return rc;
+  }
   hipStream_t s2 = side_stream();
   hipEvent_t e_fork = nullptr, e_join = nullptr;
   const bool fork = s2 != nullptr && hipEventCreateWithFlags(&e_fork, hipEventDisableTiming) == hipSuccess &&
@@ -1199,9 +1255,8 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
     io.theta = theta;
     io.out = out;
     io.pred = pred;
-    io.per = pred != nullptr ? mdfit::kNPos : 1;
-    if (int rc = launch_hpdi<true>(io, n_taxa * io.per, ws + mdfit::kHpdiCtr, hpdi_recs(workspace, n_taxa), s))
-      return rc;
+    io.per = per;
+    if (int rc = launch_hpdi<true>(io, n_taxa * io.per, hctr, recs, s, ppl == 2)) return rc;
   }
   if (fork) {
     if (hipEventRecord(e_join, s2) != hipSuccess || hipStreamWaitEvent(s, e_join, 0) != hipSuccess)
