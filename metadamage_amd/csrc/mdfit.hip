@@ -1066,7 +1066,7 @@ using mdfit::host::set_err;
 // per call, events around the whole call and around fit_kernel, on the
 // caller's stream
 constexpr int kProfMax = 256;
-constexpr int64_t kPpl2MinTaxa = 30000;  // measured crossover: 25-30k taxa
+constexpr int64_t kPpl2MinTaxa = 35000;  // measured crossover: 30-40k taxa (PPL 1 fuses the HPDI prep)
 struct ProfState {
   bool on = false;
   bool fit_only = false;  // mdfit_profile_enable(2): only the events around fit_kernel
