@@ -55,8 +55,16 @@ def main() -> None:
     for name in ("bench_trace.json", "bench_nuts_trace.json"):
         if (src / name).exists():
             shutil.copy(src / name, prof / f"{tag}_{name}")
+    # the fit kernel's hand-off as the traced bench run reports it (the record,
+    # plus at PPL 1 the fused HPDI step's wide-window list and greedy bounds)
+    handoff = None
+    try:
+        line = next(json.loads(x) for x in open(src / "bench_trace.json") if x.startswith("{"))
+        handoff = line["roofline"]["hbm_intermediate"].get("bytes_per_launch")
+    except Exception:
+        pass
     write_summary(prof, tag, "fit_kernel", TAXA, FIT_BYTES_PER_TAXON, 448, found["kernel_stats.csv"],
-                  found["pmc_fetch_size.csv"], found["pmc_write_size.csv"], "python bench.py")
+                  found["pmc_fetch_size.csv"], found["pmc_write_size.csv"], "python bench.py", handoff)
     # the NUTS chain kernel at config C3 (optional passes)
     nf, nw = sorted((src / "nuts_fetch").rglob("*counter_collection.csv")), sorted((src / "nuts_write").rglob("*counter_collection.csv"))
     if nuts and nf and nw:
@@ -67,7 +75,8 @@ def main() -> None:
                       prof / f"{tag}_nuts_pmc_write_size.csv", "python bench.py --mode nuts")
 
 
-def write_summary(prof, tag, name, taxa, bytes_per_taxon, alg_per_taxon, stats_csv, fetch_csv, write_csv, cmd):
+def write_summary(prof, tag, name, taxa, bytes_per_taxon, alg_per_taxon, stats_csv, fetch_csv, write_csv, cmd,
+                  handoff_override=None):
     k = f"mdfit::{name}" if name == "fit_kernel" else f"mdfit::nuts::{name}"
     fetch_kb = counter_mean(fetch_csv, k, "FETCH_SIZE")
     write_kb = counter_mean(write_csv, k, "WRITE_SIZE")
@@ -81,9 +90,9 @@ def write_summary(prof, tag, name, taxa, bytes_per_taxon, alg_per_taxon, stats_c
         "correction": "gfx950: FETCH_SIZE x2 (MI355X_MICROARCH.md §HBM: FETCH_SIZE reports 1/2 of wide coalesced "
         "reads; this kernel's 4-B/lane and broadcast 8-B loads are uncalibrated), WRITE_SIZE x1",
         "hbm_bytes_per_launch": int(round((2 * fetch_kb + write_kb) * 1024)),
-        "handoff_bytes_per_launch": bytes_per_taxon * taxa,
-        "handoff_note": "what the kernel moves as built (the hand-off to the next kernel: MAP the 6 sub-fit records, "
-        "NUTS the draws)",
+        "handoff_bytes_per_launch": handoff_override if handoff_override else bytes_per_taxon * taxa,
+        "handoff_note": "what the kernel moves as built (the hand-off to the next kernels: MAP the 6 sub-fit records "
+        "and, PPL 1, the fused HPDI step's wide-window list and greedy bounds; NUTS the draws)",
         "survey_algorithmic_bytes_per_launch": alg_per_taxon * taxa,
         "survey_note": "SURVEY.md 8(d): y,N in + 26 result fields out (+ 90 prediction values for NUTS)",
         "rocprof_avg_ns": float(fk.get("AverageNs", "nan")),
