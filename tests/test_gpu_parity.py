@@ -295,9 +295,11 @@ def test_bench_size_properties(engine, oracle_lib):
 
 
 def test_lane_layouts_are_bitwise_identical(engine, monkeypatch):
-    """The fit kernel's two lane layouts (1 point per lane below 30k taxa, 2
+    """The fit kernel's two lane layouts (1 point per lane below 35k taxa, 2
     above) sum in the same tree order, so a taxon's record does
-    not depend on the batch size that picked the layout."""
+    not depend on the batch size that picked the layout -- nor on where the
+    predictive HPDI's per-position step ran (fused into the PPL-1 fit kernel, or
+    hpdi_prep_kernel after PPL 2)."""
     from metadamage_amd.synthetic import generate
 
     b = generate(3_000, seed=11)
@@ -309,7 +311,7 @@ def test_lane_layouts_are_bitwise_identical(engine, monkeypatch):
         assert np.array_equal(a, c, equal_nan=True)
     # and a taxon fitted inside a batch above the threshold matches it too
     monkeypatch.delenv("MDFIT_FIT_PPL")
-    more = generate(28_000, seed=12)
+    more = generate(33_000, seed=12)  # 36k in all: above the 35k switch
     cat = [np.concatenate([getattr(b, f), getattr(more, f)]) for f in ("y", "N", "mm")]
     out_big, pred_big, st_big = engine.fit_batch(*cat)
     assert np.array_equal(out_big[:3_000], res["1"][0], equal_nan=True)

@@ -1,0 +1,101 @@
+"""GPU tests of the MAP call's alternative paths, each against the default
+call bit for bit:
+
+  * no predictions (pred == NULL): the predictive HPDI then runs for z = +1
+    only (the D_max_{lower,upper}_hpdi columns), in both lane layouts (the
+    fused per-position step of the PPL-1 fit kernel, hpdi_prep_kernel after
+    PPL 2);
+  * the NULL (legacy default) HIP stream, and a call from another host thread
+    (each thread forks the record assembly onto its own side stream).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test selected but no HIP device is visible")
+    return torch
+
+
+def _call(lib, ty, tN, tm, T, opts, res, stream_handle):
+    from metadamage_amd import _lib
+
+    _lib.check(lib.mdfit_fit_batch(
+        ctypes.c_void_p(ty.data_ptr()), ctypes.c_void_p(tN.data_ptr()), ctypes.c_void_p(tm.data_ptr()), T,
+        ctypes.byref(opts), ctypes.c_void_p(res.out.data_ptr()),
+        ctypes.c_void_p(res.pred.data_ptr()) if res.pred is not None else None,
+        ctypes.c_void_p(res.status.data_ptr()), ctypes.c_void_p(res.workspace.data_ptr()), stream_handle))
+
+
+@pytest.mark.parametrize("ppl", ["1", "2"])
+def test_without_predictions_same_record(torch_dev, monkeypatch, ppl):
+    torch = torch_dev
+    from metadamage_amd import _lib, engine
+    from metadamage_amd.synthetic import generate
+
+    monkeypatch.setenv("MDFIT_FIT_PPL", ppl)
+    b = generate(2_000, seed=21)
+    ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm)
+    opts = _lib.default_opts()
+    full = engine.fit_batch_device(ty, tN, tm, opts)
+    bare = engine.fit_batch_device(ty, tN, tm, opts, engine.alloc_outputs(2_000, with_pred=False, opts=opts))
+    torch.cuda.synchronize()
+    a, c = full.out.cpu().numpy()[:, :25], bare.out.cpu().numpy()[:, :25]
+    assert np.array_equal(a, c, equal_nan=True)  # the HPDI columns included
+    assert np.isfinite(a[:, 2:4]).mean() > 0.99
+    assert np.array_equal(full.status.cpu().numpy(), bare.status.cpu().numpy())
+
+
+def test_null_stream_and_worker_thread(torch_dev):
+    torch = torch_dev
+    from metadamage_amd import _lib, engine
+    from metadamage_amd.synthetic import generate
+
+    T = 3_000
+    b = generate(T, seed=22)
+    ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm)
+    opts = _lib.default_opts()
+    ref = engine.fit_batch_device(ty, tN, tm, opts)
+    torch.cuda.synchronize()
+    lib = _lib.load()
+    outs = []
+    # the NULL stream
+    r0 = engine.alloc_outputs(T, opts=opts)
+    _call(lib, ty, tN, tm, T, opts, r0, None)
+    torch.cuda.synchronize()
+    outs.append(r0)
+    # another host thread, on a stream of its own
+
+    def worker(box):
+        try:
+            s = torch.cuda.Stream()
+            r = engine.alloc_outputs(T, opts=opts)
+            torch.cuda.synchronize()
+            _call(lib, ty, tN, tm, T, opts, r, ctypes.c_void_p(s.cuda_stream))
+            s.synchronize()
+            box.append(r)
+        except Exception as e:  # reported in the main thread
+            box.append(e)
+
+    box: list = []
+    th = threading.Thread(target=worker, args=(box,))
+    th.start()
+    th.join(timeout=120)
+    assert box and not isinstance(box[0], Exception), box
+    outs.append(box[0])
+    for r in outs:
+        assert np.array_equal(r.out.cpu().numpy()[:, :32], ref.out.cpu().numpy()[:, :32], equal_nan=True)
+        assert np.array_equal(r.pred.cpu().numpy(), ref.pred.cpu().numpy(), equal_nan=True)
+        assert np.array_equal(r.status.cpu().numpy(), ref.status.cpu().numpy())
