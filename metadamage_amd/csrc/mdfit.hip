@@ -1092,16 +1092,29 @@ mdfit::hpdi::WideRec* hpdi_recs(void* ws, int64_t n_theta) {
 }
 
 // The side stream of mdfit_fit_batch's fork (the record assembly runs there
-// beside the HPDI kernels): one per host thread and device, created on first
-// use, non-blocking (ordered against the caller's stream by events only).
-hipStream_t side_stream() {
+// beside the HPDI kernels) and its fork / join events: one set per host thread
+// and device, created on first use; the stream non-blocking (ordered against
+// the caller's stream by the events only).  Reusing the events across calls is
+// stream-ordered (a wait binds to the record enqueued before it).
+struct Fork {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+Fork* side_fork() {
   constexpr int kMaxDev = 64;
-  static thread_local hipStream_t side[kMaxDev] = {};
+  static thread_local Fork f[kMaxDev];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
-  if (side[dev] == nullptr && hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking) != hipSuccess)
-    side[dev] = nullptr;
-  return side[dev];
+  Fork& x = f[dev];
+  if (x.s == nullptr) {
+    if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess) {
+      x = Fork{};
+      return nullptr;
+    }
+  }
+  return &x;
 }
 
 // K4a (unless the fit kernel did its work: prep = false) and K4b
@@ -1240,12 +1253,10 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
                        out, theta);
     if (int rc = check_launch("theta_kernel")) return rc;
   }
-  hipStream_t s2 = side_stream();
-  hipEvent_t e_fork = nullptr, e_join = nullptr;
-  const bool fork = s2 != nullptr && hipEventCreateWithFlags(&e_fork, hipEventDisableTiming) == hipSuccess &&
-                    hipEventCreateWithFlags(&e_join, hipEventDisableTiming) == hipSuccess &&
-                    hipEventRecord(e_fork, s) == hipSuccess && hipStreamWaitEvent(s2, e_fork, 0) == hipSuccess;
-  hipStream_t sa = fork ? s2 : s;  // no side stream: everything in order on s
+  Fork* fk = side_fork();
+  const bool fork =
+      fk != nullptr && hipEventRecord(fk->fork, s) == hipSuccess && hipStreamWaitEvent(fk->s, fk->fork, 0) == hipSuccess;
+  hipStream_t sa = fork ? fk->s : s;  // no side stream: everything in order on s
   hipLaunchKernelGGL(mdfit::assemble_kernel, dim3((unsigned)n_taxa), dim3(mdfit::kWave), 0, sa, y, N,
                      mm, n_taxa, out, pred, status);
   if (int rc = check_launch("assemble_kernel")) return rc;
@@ -1259,11 +1270,9 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
     if (int rc = launch_hpdi<true>(io, n_taxa * io.per, hctr, recs, s, ppl == 2)) return rc;
   }
   if (fork) {
-    if (hipEventRecord(e_join, s2) != hipSuccess || hipStreamWaitEvent(s, e_join, 0) != hipSuccess)
+    if (hipEventRecord(fk->join, fk->s) != hipSuccess || hipStreamWaitEvent(s, fk->join, 0) != hipSuccess)
       return set_err(MDFIT_E_HIP, "stream join");
   }
-  if (e_fork) (void)hipEventDestroy(e_fork);  // released once complete
-  if (e_join) (void)hipEventDestroy(e_join);
   prof_record(3, s);
   if (g_prof.on && g_prof.n < kProfMax) ++g_prof.n;
   return 0;

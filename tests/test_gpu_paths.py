@@ -99,3 +99,32 @@ def test_null_stream_and_worker_thread(torch_dev):
         assert np.array_equal(r.out.cpu().numpy()[:, :32], ref.out.cpu().numpy()[:, :32], equal_nan=True)
         assert np.array_equal(r.pred.cpu().numpy(), ref.pred.cpu().numpy(), equal_nan=True)
         assert np.array_equal(r.status.cpu().numpy(), ref.status.cpu().numpy())
+
+
+def test_graph_capture_of_the_call(torch_dev):
+    """The MAP call (with its side-stream fork / join) captured into a HIP graph
+    on the caller's stream and replayed: the same record as a direct call."""
+    torch = torch_dev
+    from metadamage_amd import _lib, engine
+    from metadamage_amd.synthetic import generate
+
+    T = 2_000
+    b = generate(T, seed=23)
+    ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm)
+    opts = _lib.default_opts()
+    ref = engine.fit_batch_device(ty, tN, tm, opts)
+    torch.cuda.synchronize()
+    lib = _lib.load()
+    r = engine.alloc_outputs(T, opts=opts)
+    s = torch.cuda.Stream()
+    _call(lib, ty, tN, tm, T, opts, r, ctypes.c_void_p(s.cuda_stream))  # warm (side stream created)
+    s.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        _call(lib, ty, tN, tm, T, opts, r, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    for _ in range(2):
+        r.out.fill_(0.0)
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(r.out.cpu().numpy()[:, :32], ref.out.cpu().numpy()[:, :32], equal_nan=True)
+        assert np.array_equal(r.pred.cpu().numpy(), ref.pred.cpu().numpy(), equal_nan=True)
