@@ -6,7 +6,10 @@ call bit for bit:
     fused per-position step of the PPL-1 fit kernel, hpdi_prep_kernel after
     PPL 2);
   * the NULL (legacy default) HIP stream, and a call from another host thread
-    (each thread forks the record assembly onto its own side stream).
+    (each thread forks the record assembly onto its own side stream);
+  * the call captured into a HIP graph and replayed;
+  * garbage-filled workspace and outputs (MAP in both layouts, NUTS): every
+    record column equal to a call on zeroed buffers.
 """
 
 from __future__ import annotations
@@ -128,3 +131,43 @@ def test_graph_capture_of_the_call(torch_dev):
         torch.cuda.synchronize()
         assert np.array_equal(r.out.cpu().numpy()[:, :32], ref.out.cpu().numpy()[:, :32], equal_nan=True)
         assert np.array_equal(r.pred.cpu().numpy(), ref.pred.cpu().numpy(), equal_nan=True)
+
+
+@pytest.mark.parametrize("mode,ppl", [("map", "1"), ("map", "2"), ("nuts", "1")])
+def test_dirty_workspace_and_outputs(torch_dev, monkeypatch, mode, ppl):
+    """The library never assumes a clean workspace (torch.empty, reused across
+    calls and sizes) or clean outputs: every counter, list and draw buffer it
+    reads is written first in the call.  Garbage-filled workspace and outputs
+    give the record of a call on zeroed ones, bit for bit."""
+    torch = torch_dev
+    from metadamage_amd import _lib, engine
+    from metadamage_amd.synthetic import generate
+
+    monkeypatch.setenv("MDFIT_FIT_PPL", ppl)
+    T = 1_500 if mode == "map" else 96
+    b = generate(T, seed=24)
+    ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm)
+    opts = _lib.default_opts(mode=_lib.MODE_NUTS if mode == "nuts" else _lib.MODE_MAP)
+    if mode == "nuts":
+        opts.num_warmup, opts.num_samples = 60, 80
+    lib = _lib.load()
+    clean = engine.alloc_outputs(T, opts=opts)
+    clean.workspace.zero_()
+    clean.out.zero_()
+    clean.pred.zero_()
+    clean.status.zero_()
+    _call(lib, ty, tN, tm, T, opts, clean, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    dirty = engine.alloc_outputs(T, opts=opts)
+    g = torch.Generator(device="cpu").manual_seed(7)
+    for _ in range(2):  # second round: the workspace as the first call left it, outputs re-dirtied
+        dirty.out.copy_(torch.randn(dirty.out.shape, generator=g, dtype=dirty.out.dtype) * 1e30)
+        dirty.pred.fill_(float("nan"))
+        dirty.status.fill_(-7)
+        if _ == 0:
+            dirty.workspace.copy_(torch.randint(0, 256, dirty.workspace.shape, generator=g, dtype=torch.uint8))
+        _call(lib, ty, tN, tm, T, opts, dirty, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        torch.cuda.synchronize()
+        # every column of the record, the per-sub-fit diagnostics included
+        assert np.array_equal(dirty.out.cpu().numpy(), clean.out.cpu().numpy(), equal_nan=True)
+        assert np.array_equal(dirty.pred.cpu().numpy(), clean.pred.cpu().numpy(), equal_nan=True)
+        assert np.array_equal(dirty.status.cpu().numpy(), clean.status.cpu().numpy())
