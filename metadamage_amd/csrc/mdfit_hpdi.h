@@ -39,6 +39,12 @@ namespace hpdi {
 #ifndef MDFIT_HPDI_UNROLL
 #define MDFIT_HPDI_UNROLL 1
 #endif
+#ifndef MDFIT_HPDI_FLAT_ROOT
+#define MDFIT_HPDI_FLAT_ROOT 1  // the two ends' Newton root steps as one per-lane loop (wide_iter)
+#endif
+#ifndef MDFIT_HPDI_FLAT_GL
+#define MDFIT_HPDI_FLAT_GL 1  // the Gauss-Legendre panels as one per-lane loop (wide_mass)
+#endif
 
 // diagnostic builds only (-DMDFIT_HPDI_COUNT): per site k, lane executions
 // [2k] and wave issues [2k+1] -- the SIMD efficiency of the loops
@@ -299,6 +305,70 @@ __device__ __forceinline__ double wide_mass(const Pmf& P, double A, double B, do
   if (B1 < A1) return tot;
   const double c = fmin(fmax(P.m, A1), B1);
   double I = 0.0;
+#if MDFIT_HPDI_FLAT_GL
+  // The same panels and nodes in the same order (part, panel, node), as ONE
+  // per-lane loop: a wave issues the largest per-lane node count instead of
+  // the sum over parts of the largest panel counts.  Part setup when a lane
+  // enters its next non-empty part.
+  double v0 = 0.0, dv = 0.0, acc = 0.0;
+  bool lg = false, snl = false;
+  int kp = 0, j = 0, nd = 0, pi = 0;
+  auto setup = [&](int q) -> bool {
+    const int part = q >> 1, sub = q & 1;
+    const double u0 = part == 0 ? A1 : c, u1 = part == 0 ? c : B1;
+    if (!(u1 > u0)) return false;
+    const double L = u1 - u0;
+    const bool nl = (u0 + P.a) < L, nr = (N - u1 + P.b) < L;
+    double a0 = u0, a1 = u1;
+    bool snl_ = nl, snr = nr;
+    if (nl && nr) {
+      const double cm = 0.5 * (u0 + u1), L2 = cm - u0;
+      if (sub == 0) {
+        a1 = cm;
+        snl_ = (u0 + P.a) < L2;
+        snr = false;
+      } else {
+        a0 = cm;
+        snl_ = false;
+        snr = (N - u1 + P.b) < L2;
+      }
+    } else if (sub == 1) {
+      return false;
+    }
+    lg = snl_ || snr;
+    snl = snl_;
+    v0 = lg ? (snl_ ? flog(a0 + P.a) : flog(N - a1 + P.b)) : a0;
+    const double v1 = lg ? (snl_ ? flog(a1 + P.a) : flog(N - a0 + P.b)) : a1;
+    int k = lg ? (int)ceil((v1 - v0) / kLV) : (int)ceil((a1 - a0) / (kLX * sd));
+    kp = k < 1 ? 1 : k;
+    dv = (v1 - v0) / kp;
+    return true;
+  };
+  bool have = false;
+  while (pi < 4 && !(have = setup(pi))) ++pi;
+  while (have) {
+    const double w0 = v0 + dv * j, w1 = v0 + dv * (j + 1);
+    const double h = 0.5 * (w1 - w0), cc = 0.5 * (w1 + w0);
+    const double gx = nd < 3 ? -kGLX[2 - nd] : kGLX[nd - 3];
+    const double gw = kGLW[nd < 3 ? 2 - nd : nd - 3];
+    HPDI_CNT(2);
+    const double v = cc + h * gx;
+    const double ev = lg ? fexp(v) : 1.0;
+    const double x = lg ? (snl ? ev - P.a : N + P.b - ev) : v;
+    acc += gw * ev * fexp(g_of(P, x));
+    if (++nd == 6) {
+      I += h * acc;
+      acc = 0.0;
+      nd = 0;
+      if (++j == kp) {
+        j = 0;
+        have = false;
+        while (++pi < 4 && !(have = setup(pi))) {
+        }
+      }
+    }
+  }
+#else
   // parts [A1, c], [c, B1]; a part near both support ends splits at its midpoint
   for (int pi = 0; pi < 4; ++pi) {
     const int part = pi >> 1, sub = pi & 1;
@@ -345,6 +415,7 @@ __device__ __forceinline__ double wide_mass(const Pmf& P, double A, double B, do
       I += h * acc;
     }
   }
+#endif
   // Euler-Maclaurin ends: one site for both
   double fe[2], se[2];
 #pragma unroll 1
@@ -476,6 +547,50 @@ __device__ __forceinline__ bool wide_iter(Wide& W) {
     cl = m == 0.0 || W.g0 >= t;
     cr = m == N || W.gN >= t;
     // the free ends' roots of g = t (oracle: hp_root): one site for both
+#if MDFIT_HPDI_FLAT_ROOT
+    // both ends' Newton steps as ONE per-lane loop (end 0's steps, then end
+    // 1's: the same arithmetic per end), so a wave issues the largest per-lane
+    // total instead of the sum of the per-end maxima
+    int e = cl ? (cr ? 2 : 1) : 0;
+    if (cl) xe[0] = 0.0;
+    double rlo = 0.0, rhi = m, xr = 0.0;
+    bool rising = true;
+    int k = 0;
+    auto start_end = [&](int ee) {
+      rlo = ee == 0 ? 0.0 : m;
+      rhi = ee == 0 ? m : N;
+      rising = ee == 0;
+      xr = fmin(fmax(ee == 0 ? xe[0] : xe[1], rlo), rhi);
+      k = 0;
+    };
+    if (e < 2) start_end(e);
+    while (e < 2) {
+      double sx;
+      HPDI_CNT(1);
+      const double gx = gfun<true>(P, xr, sx) - t;
+      bool fin = fabs(gx) < 1e-12;
+      if (!fin) {
+        if ((gx < 0.0) == rising) rlo = xr;
+        else rhi = xr;
+        double xn = sx != 0.0 ? xr - gx / sx : 0.5 * (rlo + rhi);
+        if (!(rlo < xn && xn < rhi)) xn = 0.5 * (rlo + rhi);
+        const bool conv = fabs(xn - xr) < 0.05;
+        xr = xn;
+        fin = conv || ++k >= 60;
+      }
+      if (fin) {
+        if (e == 0) {
+          xe[0] = xr;
+          e = cr ? 2 : 1;
+          if (e == 1) start_end(1);
+        } else {
+          xe[1] = xr;
+          e = 2;
+        }
+      }
+    }
+    if (cr) xe[1] = N;
+#else
 #pragma unroll 1
     for (int e = 0; e < 2; ++e) {
       const bool clamped = e == 0 ? cl : cr;
@@ -501,6 +616,7 @@ __device__ __forceinline__ bool wide_iter(Wide& W) {
       }
       xe[e] = xr;
     }
+#endif
     W.xe0 = xe[0];
     W.xe1 = xe[1];
     A = ceil(xe[0]);
