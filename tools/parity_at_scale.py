@@ -5,6 +5,7 @@ metric (|gpu - cpu| / max(|cpu|, 1e-2) over taxa both fitted) and the status
 agreement, as one JSON line per size.
 
     python tools/parity_at_scale.py > profiles/r01_parity_at_scale.jsonl
+    python tools/parity_at_scale.py --sizes 1000000:4   # C4's whole 1M taxa on one GPU
 """
 
 from __future__ import annotations
@@ -22,7 +23,17 @@ sys.path.insert(0, str(ROOT))
 
 
 def main() -> None:
+    import argparse
+
     import torch
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sizes", nargs="*", default=None, help="TAXA:SEED pairs (default: C2, C3 size, C4 share)")
+    a = ap.parse_args()
+    sizes = ((10_000, 1, "C2"), (100_000, 2, "C3 size, MAP"), (125_000, 3, "C4 per-GPU share"))
+    if a.sizes:
+        sizes = tuple((int(t), int(sd), "C4 whole (1M taxa)" if int(t) == 1_000_000 else f"{t} taxa")
+                      for t, sd in (x.split(":") for x in a.sizes))
 
     from bench import parity
     from metadamage_amd import engine
@@ -31,12 +42,22 @@ def main() -> None:
 
     oracle = OracleLib()
     threads = min(16, os.cpu_count() or 1)
-    for T, seed, label in ((10_000, 1, "C2"), (100_000, 2, "C3 size, MAP"), (125_000, 3, "C4 per-GPU share")):
+    for T, seed, label in sizes:
         b = generate(T, seed=seed)
+        print(f"generated {T} taxa", file=sys.stderr, flush=True)
         out, pred, st = engine.fit_batch(b.y, b.N, b.mm)
         torch.cuda.synchronize()
+        print(f"GPU fit of {T} taxa done", file=sys.stderr, flush=True)
         t0 = time.perf_counter()
-        ref, rpred, rst = oracle.fit_batch(b.y, b.N, b.mm, threads=threads)
+        # in 100k-taxon pieces with a progress line each (taxa are independent,
+        # so the pieces give the same records; a silent multi-minute call reads
+        # as a hang to the GPU runner)
+        parts = []
+        for lo in range(0, T, 100_000):
+            hi = min(T, lo + 100_000)
+            parts.append(oracle.fit_batch(b.y[lo:hi], b.N[lo:hi], b.mm[lo:hi], threads=threads))
+            print(f"oracle {hi}/{T} taxa, {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+        ref, rpred, rst = (np.concatenate([q[i] for q in parts]) for i in range(3))
         cpu_s = time.perf_counter() - t0
         line = parity(out, st, ref, rst, kind="MAP, same MDFIT-MAP v1 as the oracle")
         line.update(config=label, n_taxa=T, seed=seed, gpu_status_ok=float((st == 0).mean()),
@@ -45,6 +66,7 @@ def main() -> None:
                     pred_max_abs=float(np.nanmax(np.abs(pred - rpred))), oracle_s=round(cpu_s, 2),
                     oracle_threads=threads)
         print(json.dumps(line), flush=True)
+        del b, out, pred, st, ref, rpred, rst
 
 
 if __name__ == "__main__":
