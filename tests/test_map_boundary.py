@@ -1,9 +1,10 @@
 """MAP fits whose optimum sits at or just inside a box bound (synthetic C5 /
 C3 taxa that once ended in MDFIT_MAXITER): phi creeping to its lower bound
 along the flat exp tail of u3, and an interior c optimum 6e-5 above c = 0 that
-the old epsilon-active set pinned to the bound.  Both must converge (status
-OK) to a point no feasible nearby point improves on, in the oracle (CPU) and
-in the HIP kernel (GPU, against the oracle)."""
+the old epsilon-active set pinned to the bound; plus the flat-valley taxa of
+the 1M-taxon parity run (GPU and oracle stop at different points of equal F).
+All must converge (status OK) to a point no feasible nearby point improves on,
+in the oracle (CPU) and in the HIP kernel (GPU, against the oracle)."""
 
 from __future__ import annotations
 
@@ -95,9 +96,11 @@ def test_kernel_converges_at_bounds_like_the_oracle(oracle_lib):
         if rel < RTOL:
             continue
         # a flat valley (c5_102058064: q moves 7.7e-4 while F changes below its
-        # rounding scale): then the GPU's modes must be optimal
-        # to F's resolution -- the oracle's objective at them within its own
-        # optimum's rounding scale -- for every sub-fit
+        # rounding scale; the five m1_* taxa of the 1M-taxon
+        # parity run, up to 1.45e-3 on q_mean for m1_t839013): then
+        # the GPU's modes must be optimal to F's resolution -- the oracle's
+        # objective at them within its own optimum's rounding scale -- for
+        # every sub-fit
         for s, (model, subset) in enumerate(kinds):
             q, A, c, phi = out[i, 32 + 8 * s: 36 + 8 * s]
             u = np.array([np.log(q / (1 - q)), np.log(A / (1 - A)) if model == 0 else 0.0,
@@ -105,4 +108,4 @@ def test_kernel_converges_at_bounds_like_the_oracle(oracle_lib):
             Fg = oracle_lib.objective(model, subset, y[i, :30], N[i, :30], u)[0]
             Fo = ref[i, 32 + 8 * s + 4]
             assert Fg <= Fo + 1.4e-14 * 1e3 * abs(Fo) + 1e-9, (name, s, Fg - Fo)
-        assert rel < 1e-3, (name, rel)
+        assert rel < 2e-3, (name, rel)

@@ -29,6 +29,7 @@ def main() -> None:
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", nargs="*", default=None, help="TAXA:SEED pairs (default: C2, C3 size, C4 share)")
+    ap.add_argument("--dump", default=None, help="npz path: the 16 taxa furthest from the oracle, inputs + both records")
     a = ap.parse_args()
     sizes = ((10_000, 1, "C2"), (100_000, 2, "C3 size, MAP"), (125_000, 3, "C4 per-GPU share"))
     if a.sizes:
@@ -66,6 +67,12 @@ def main() -> None:
                     pred_max_abs=float(np.nanmax(np.abs(pred - rpred))), oracle_s=round(cpu_s, 2),
                     oracle_threads=threads)
         print(json.dumps(line), flush=True)
+        if a.dump:
+            rel = np.abs(out[:, :25] - ref[:, :25]) / np.maximum(np.abs(ref[:, :25]), 1e-2)
+            rel = np.where(np.isnan(out[:, :25]) & np.isnan(ref[:, :25]), 0.0, rel).max(axis=1)
+            idx = np.argsort(-np.nan_to_num(rel, nan=np.inf))[:16]
+            np.savez(a.dump, idx=idx, rel=rel[idx], y=b.y[idx], N=b.N[idx], mm=b.mm[idx], gpu=out[idx], cpu=ref[idx],
+                     gpu_status=st[idx], cpu_status=rst[idx])
         del b, out, pred, st, ref, rpred, rst
 
 
