@@ -97,7 +97,12 @@ enum mdfit_field {
   MDFIT_NRESULT, /* = 25 result columns */
   /* diagnostics: sub-fit k in {0 PMD-all, 1 null-all, 2 PMD-fwd, 3 PMD-rev,
    * 4 null-fwd, 5 null-rev} occupies MDFIT_F_DIAG + 8*k + {q, A, c, phi,
-   * objective, evaluations, status, unused}.  Null sub-fits store A = c = 0. */
+   * objective, evaluations, status, polished}.  Null sub-fits store A = c = 0.
+   * MAP: `polished` = 1 when the fit entered its polish phase (DESIGN.md
+   * §3.4); its objective is then the cancellation-free form (the full log-pmf,
+   * log C(N,y) included), else the lnGamma-sum form.  NUTS: {posterior means
+   * of q, A, c, phi, adapted step size, leapfrogs per draw, status,
+   * divergences}. */
   MDFIT_F_DIAG = 32,
   MDFIT_NOUT = 80
 };
@@ -131,11 +136,14 @@ void mdfit_default_opts(mdfit_opts* opts);
  *   pred      : float[n_taxa][MDFIT_NPRED][MDFIT_NPOS] or NULL (device)
  *   status    : int32_t[n_taxa]                             (device)
  *   workspace : device buffer of mdfit_workspace_bytes(n_taxa) bytes (work
- *               queues, the PMD-all mode for the HPDI, the wide-window list)
+ *               queues, the PMD-all mode for the HPDI, the wide-window list:
+ *               MAP 256 B + 4,832 B per taxon)
  *   hip_stream: hipStream_t or NULL.  MAP: the record assembly runs on a
- *               library-owned side stream (one per host thread and device),
- *               forked from and joined back into hip_stream by events, so the
- *               call stays ordered on hip_stream and capturable in a graph
+ *               library-owned side stream (one per device, created once),
+ *               forked from and joined back into hip_stream by events on every
+ *               return path, so the call stays ordered on hip_stream and
+ *               capturable in a graph
+ *   n_taxa    : at most 2^25 per call (MAP: int32 position indices)
  * Replaces compute_fits' per-taxon loop (fits.py:477-526, 569-626, 709-730).
  */
 int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm,

@@ -81,13 +81,9 @@ def cli_fit(
     # launched by torchrun (WORLD_SIZE > 1): one rank per GPU, the rank's GPU
     # selected before any device call, RCCL process group; main() then deals
     # files or shards taxa over the ranks and rank 0 writes the shared results
-    from .distributed import init_from_env, shutdown
+    from .distributed import run_distributed
 
-    init_from_env()
-    try:
-        main(filenames, cfg)
-    finally:
-        shutdown()
+    run_distributed(main, filenames, cfg)
 
 
 @cli_app.command("dashboard")

@@ -35,6 +35,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 
 #include "../../include/mdfit.h"
 #include "mdfit_hpdi.h"
@@ -159,8 +160,10 @@ constexpr int kPrioEvals = 15;  // fit length (evaluations) that raises the wave
 // current point, re-evaluation pending, escape line search running,
 // exhaustion status OK, the escape count (kEscCount, in units of kEscN: at
 // most 4); the flat-tail rescue done / its relaxed acceptance pending
+// the polish phase: F in the cancellation-free form from here on / its
+// re-evaluation at u pending
 constexpr unsigned kEscIndef = 1u, kEscProbe = 2u, kEscNc = 4u, kEscExhOk = 8u, kEscN = 16u, kEscCount = 0x70u,
-                   kEscRescued = 0x100u, kEscRelax = 0x200u;
+                   kEscRescued = 0x100u, kEscRelax = 0x200u, kEscPolish = 0x400u, kEscPolishProbe = 0x800u;
 
 // ---------------------------------------------------------------------------
 // The predictive HPDI's per-position step (K4a, and the fused prep of the PPL-1
@@ -417,8 +420,9 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
     double acc[kNAcc];
 #pragma unroll
     for (int j = 0; j < kNAcc; ++j) acc[j] = 0.0;
+    const int accf = (esc & kEscPolish) != 0u;
     if (PPL == 1) {
-      point_accum<true>(pa, th, acc);
+      point_accum<true>(pa, th, acc, accf);
     } else {
       // lg3(phi) from a pad: lane 15's point b (all-position: both halves;
       // pair: the reverse half), lane 7's point b (pair: the forward half)
@@ -428,11 +432,11 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       t6.l = src15 ? rowb<15>(t3b.l) : rowb<7>(t3b.l);
       t6.p = src15 ? rowb<15>(t3b.p) : rowb<7>(t3b.p);
       t6.q = src15 ? rowb<15>(t3b.q) : rowb<7>(t3b.q);
-      point_contrib(pa, th, lg3(pa.N + th.phi), t6, acc);
+      point_contrib(pa, th, lg3(pa.N + th.phi), t6, acc, accf);
       double accb[kNAcc];
 #pragma unroll
       for (int j = 0; j < kNAcc; ++j) accb[j] = 0.0;
-      point_contrib(pb, th, t3b, t6, accb);
+      point_contrib(pb, th, t3b, t6, accb, accf);
 #pragma unroll
       for (int j = 0; j < kNAcc; ++j) acc[j] = opaque(acc[j]) + opaque(accb[j]);
     }
@@ -466,8 +470,11 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       // the saddle escape's re-evaluation at u (same F, g, H as the current
       // point) goes through the acceptance below; its H gives the direction
       const bool probed = esc & kEscProbe;
-      esc &= ~kEscProbe;
-      if (probed) {
+      // the polish phase's re-evaluation at u (F now in the other form): taken
+      // as the current point, then the ordinary Newton step (the same d)
+      const bool pprobe = esc & kEscPolishProbe;
+      esc &= ~(kEscProbe | kEscPolishProbe);
+      if (probed || pprobe) {
         accept = true;
       } else if (first) {
         accept = true;
@@ -517,7 +524,15 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         }
       } else {
         t *= 0.5;
-        if (t < 1e-12) {  // line search exhausted (oracle: fit_one)
+        if (!(esc & kEscPolish) && evals < max_iter &&
+            (t < 1e-12 || t * fabs(curGd) <= kNoiseF * (curMag + fabs(curF)))) {
+          // the polish phase (oracle: fit_one): the backtracking step's
+          // predicted decrease is below F's rounding -- re-evaluate at u with F
+          // in the cancellation-free form next trip, then restart at t = 1
+          esc |= kEscPolish | kEscPolishProbe;
+          d[0] = d[1] = d[2] = d[3] = 0.0;
+          t = 1.0;
+        } else if (t < 1e-12) {  // line search exhausted (oracle: fit_one)
           if (!(esc & kEscRescued) && u[3] < 0.0 && d[3] < 0.0 && u[3] > kULo[3]) {
             // the flat tail of log delta: jump onto its lower bound once
             esc |= kEscRescued | kEscRelax;
@@ -555,7 +570,9 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         const bool writer = (!whole || h == 0) && i < 8;
         if (writer) {
           const double v = i < 4 ? sel4(u, i)
-                                 : (i == 4 ? curF : (i == 5 ? (double)evals : (i == 6 ? (double)status : 0.0)));
+                                 : (i == 4 ? curF
+                                           : (i == 5 ? (double)evals
+                                                     : (i == 6 ? (double)status : ((esc & kEscPolish) ? 1.0 : 0.0))));
           diag(out, taxon, sub)[i] = v;
         }
         allok = status == MDFIT_OK;  // (read after an all-position fit: the pair's warm start)
@@ -1092,30 +1109,66 @@ mdfit::hpdi::WideRec* hpdi_recs(void* ws, int64_t n_theta) {
 }
 
 // The side stream of mdfit_fit_batch's fork (the record assembly runs there
-// beside the HPDI kernels) and its fork / join events: one set per host thread
-// and device, created on first use; the stream non-blocking (ordered against
-// the caller's stream by the events only).  Reusing the events across calls is
-// stream-ordered (a wait binds to the record enqueued before it).
+// beside the HPDI kernels) and its fork / join events: one set per device,
+// created on first use and kept for the process (a bounded 1 stream per
+// device, not one per calling host thread); the stream non-blocking (ordered
+// against the caller's stream by the events only).  The events are shared, so
+// a call holds the device's mutex from the fork record to the join wait: a
+// wait binds to the record enqueued before it, and another thread's record in
+// between would rebind it.
 struct Fork {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  std::mutex mu;
 };
 Fork* side_fork() {
   constexpr int kMaxDev = 64;
-  static thread_local Fork f[kMaxDev];
+  static Fork f[kMaxDev];
+  static std::mutex make_mu;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
   Fork& x = f[dev];
+  std::lock_guard<std::mutex> g(make_mu);
   if (x.s == nullptr) {
-    if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess ||
+    if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess) {
-      x = Fork{};
+      (void)hipStreamDestroy(x.s);
+      if (x.fork) (void)hipEventDestroy(x.fork);
+      x.s = nullptr;
+      x.fork = x.join = nullptr;
       return nullptr;
     }
   }
   return &x;
 }
+
+// The fork's scope: holds the device's fork mutex and, when the fork was
+// opened, joins the side stream back into the caller's stream on EVERY exit
+// of mdfit_fit_batch -- error returns included -- so no kernel of the call is
+// still running on the side stream when the caller (whose allocator orders
+// frees against its own stream only) gets control back, and a graph capture
+// never ends with an open fork.
+struct ForkScope {
+  Fork* fk;
+  hipStream_t s;
+  bool open = false;
+  std::unique_lock<std::mutex> lk;
+  ForkScope(Fork* f, hipStream_t st) : fk(f), s(st) {
+    if (fk == nullptr) return;
+    lk = std::unique_lock<std::mutex>(fk->mu);
+    open = hipEventRecord(fk->fork, s) == hipSuccess && hipStreamWaitEvent(fk->s, fk->fork, 0) == hipSuccess;
+  }
+  hipStream_t side() const { return open ? fk->s : s; }  // no side stream: everything in order on s
+  int join() {
+    if (!open) return 0;
+    open = false;
+    if (hipEventRecord(fk->join, fk->s) != hipSuccess || hipStreamWaitEvent(s, fk->join, 0) != hipSuccess)
+      return set_err(MDFIT_E_HIP, "stream join");
+    return 0;
+  }
+  ~ForkScope() { (void)join(); }
+};
 
 // K4a (unless the fit kernel did its work: prep = false) and K4b
 template <bool kFit>
@@ -1208,7 +1261,10 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   if (opts) o = *opts;
   if (o.mode != MDFIT_MODE_MAP && o.mode != MDFIT_MODE_NUTS) return set_err(MDFIT_E_ARG, "unsupported mode");
   if (o.max_iter < 1) return set_err(MDFIT_E_ARG, "max_iter < 1");
-  if (n_taxa > ((int64_t)1 << 29)) return set_err(MDFIT_E_ARG, "n_taxa exceeds 2^29 per call");
+  // the HPDI list counters and indices are int32 over T * 30 positions, and the
+  // MAP workspace holds ~4.8 KB per taxon (mdfit_workspace_bytes): 2^25 taxa
+  // (1e9 positions, ~162 GB of workspace) per call at most
+  if (n_taxa > ((int64_t)1 << 25)) return set_err(MDFIT_E_ARG, "n_taxa exceeds 2^25 per call");
   hipStream_t s = (hipStream_t)hip_stream;
   int* ws = (int*)workspace;
   prof_record(0, s);
@@ -1253,10 +1309,8 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
                        out, theta);
     if (int rc = check_launch("theta_kernel")) return rc;
   }
-  Fork* fk = side_fork();
-  const bool fork =
-      fk != nullptr && hipEventRecord(fk->fork, s) == hipSuccess && hipStreamWaitEvent(fk->s, fk->fork, 0) == hipSuccess;
-  hipStream_t sa = fork ? fk->s : s;  // no side stream: everything in order on s
+  ForkScope fork(side_fork(), s);
+  hipStream_t sa = fork.side();
   hipLaunchKernelGGL(mdfit::assemble_kernel, dim3((unsigned)n_taxa), dim3(mdfit::kWave), 0, sa, y, N,
                      mm, n_taxa, out, pred, status);
   if (int rc = check_launch("assemble_kernel")) return rc;
@@ -1269,10 +1323,7 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
     io.per = per;
     if (int rc = launch_hpdi<true>(io, n_taxa * io.per, hctr, recs, s, ppl == 2)) return rc;
   }
-  if (fork) {
-    if (hipEventRecord(fk->join, fk->s) != hipSuccess || hipStreamWaitEvent(s, fk->join, 0) != hipSuccess)
-      return set_err(MDFIT_E_HIP, "stream join");
-  }
+  if (int rc = fork.join()) return rc;
   prof_record(3, s);
   if (g_prof.on && g_prof.n < kProfMax) ++g_prof.n;
   return 0;

@@ -179,8 +179,15 @@ struct PointData {
 // oracle/mdfit_oracle.c evaluate(); derivation in DESIGN.md §3), given the
 // point's t3 = (lnGamma, psi, psi1)(N + phi) and t6 = the same at phi.
 // Returns the point's log-likelihood (without log C(N,y)).
+//
+// accf (the polish phase of the fit, oracle: evaluate(accf = 1)): the value
+// term is instead the full log-pmf in the cancellation-free form bb_logpmf_ab
+// (the objective shifts by the constant sum log C(N,y)), and the rounding scale
+// acc[1] the sum of its three |R| terms: F then resolves ~1e-10 instead of the
+// ~1e-6 of a sum of ~N ln N-sized lnGamma values.  Gradient and Hessian terms
+// are the same in both forms.
 __device__ __forceinline__ double point_contrib(const PointData& pd, const Theta& th, const LG3& t3,
-                                               const LG3& t6, double acc[kNAcc]) {
+                                               const LG3& t6, double acc[kNAcc], int accf = 0) {
   double D, Dq, DA, Dc, Dqq, DqA;
   if (pd.pmd) {
     const double kk = (double)pd.k;
@@ -212,7 +219,12 @@ __device__ __forceinline__ double point_contrib(const PointData& pd, const Theta
   mag += fabs(t2.l) + fabs(t5.l);
   const double lS = t3.l - t6.l, S = t6.p - t3.p, S1 = t6.q - t3.q;
   mag += fabs(t3.l) + fabs(t6.l);
-  const double ell = (la + lb) - lS;  // exact 0 when N = 0
+  double ell = (la + lb) - lS;  // exact 0 when N = 0
+  if (accf) {
+    const double r1 = lrise(pd.y, a), r2 = lrise(pd.N - pd.y, b), r3 = lrise(pd.N, phi);
+    ell = (r1 + r2) - r3;
+    mag = (fabs(r1) + fabs(r2)) + fabs(r3);
+  }
   const double lD = phi * (Pa - Pb);
   const double lF = D * Pa + omD * Pb + S;
   const double lDD = phi * phi * (Qa + Qb);
@@ -247,7 +259,7 @@ __device__ __forceinline__ double point_contrib(const PointData& pd, const Theta
 // lanes active, lane 15 of every row a pad holding the row's phi).
 template <bool kRowPhi = false>
 __device__ __forceinline__ double point_accum(const PointData& pd, const Theta& th,
-                                              double acc[kNAcc]) {
+                                              double acc[kNAcc], int accf = 0) {
   const LG3 t3 = lg3(pd.N + th.phi);
   LG3 t6;
   if (kRowPhi) {
@@ -257,7 +269,7 @@ __device__ __forceinline__ double point_accum(const PointData& pd, const Theta& 
   } else {
     t6 = lg3(th.phi);
   }
-  return point_contrib(pd, th, t3, t6, acc);
+  return point_contrib(pd, th, t3, t6, acc, accf);
 }
 
 // Pointwise log-likelihood of one point at a mode for the record assembly

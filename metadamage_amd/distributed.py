@@ -149,12 +149,43 @@ def init_from_env(backend: str | None = None) -> tuple[int, int]:
     return dist.get_rank(), dist.get_world_size()
 
 
-def shutdown() -> None:
+def shutdown(ok: bool = True) -> None:
+    """Leave the process group.  ok=True (the run succeeded on this rank): a
+    barrier first, so no rank tears the group down under a peer's last
+    collective.  ok=False (this rank raised): no barrier -- an NCCL barrier is
+    itself a one-element all-reduce and could pair with a healthy peer's
+    agreement all-reduce or result gather, leaving the job hung until the
+    collective timeout; the group is torn down (RCCL: the communicator
+    aborted) so the peers' pending collectives fail and the job exits."""
     import torch.distributed as dist
 
-    if dist.is_available() and dist.is_initialized():
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    if ok:
         dist.barrier()
         dist.destroy_process_group()
+        return
+    from torch.distributed import distributed_c10d as c10d
+
+    abort = getattr(c10d, "_abort_process_group", None)
+    if dist.get_backend() == "nccl" and abort is not None:
+        abort()  # tears the communicators down without waiting on peers
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def run_distributed(fn, *args, **kwargs):
+    """Join the torchrun job (init_from_env), run fn, leave the group: with a
+    barrier when fn returned, without one when it raised (shutdown(ok=False)),
+    re-raising so the launcher tears the job down."""
+    init_from_env()
+    try:
+        result = fn(*args, **kwargs)
+    except BaseException:
+        shutdown(ok=False)
+        raise
+    shutdown(ok=True)
+    return result
 
 
 def unpack_gathered(parts, n_taxa: int, world: int):

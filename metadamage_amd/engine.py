@@ -232,7 +232,8 @@ def hpdi68(N, a, b, device="cuda"):
     torch = _torch()
     lib = _lib.load()
     shape = np.broadcast(N, a, b).shape
-    ts = [torch.as_tensor(np.ascontiguousarray(np.broadcast_to(v, shape), dtype=np.float64).ravel(), device=device)
+    # np.array copies: a broadcast view is read-only (torch warns on those)
+    ts = [torch.as_tensor(np.array(np.broadcast_to(v, shape), dtype=np.float64).ravel(), device=device)
           for v in (N, a, b)]
     n = ts[0].numel()
     lo = torch.empty(n, dtype=torch.float64, device=device)

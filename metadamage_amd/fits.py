@@ -174,9 +174,10 @@ def fit_packed(p: Packed, opts=None, shard: bool = True):
     rank = dist.get_rank() if world > 1 else 0
     dev = torch.device("cuda", torch.cuda.current_device())
     # add_noise_estimates (fits.py:359-376) runs in the assembly kernel on the
-    # shipped mismatch counts: 1,440 B/taxon of asynchronous PCIe (~0.3 ms per
-    # 10k taxa) is cheaper than the host statistics (ingest.noise: ~4 ms of CPU
-    # per 10k on 8 threads) while the multi-file pipeline is host-bound
+    # shipped mismatch counts: 1,440 B/taxon of asynchronous PCIe (~0.7 ms per
+    # 10k taxa, bench host_to_host) costs no host time, while the host
+    # statistics (ingest.noise) take ~1.5 ms of CPU per 10k taxa on the 16-thread
+    # share of a multi-file pipeline that is host-bound
     if world == 1:
         return engine.fit_batch_host(p.y, p.N, p.mm, opts)
     lo, hi = shard_range(p.n_taxa, rank, world)

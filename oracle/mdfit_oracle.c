@@ -138,15 +138,27 @@ typedef struct {
   double g[4];     /* dF/du                                          */
   double H[4][4];  /* d2F/du2                                        */
   double mag;      /* sum |lgamma terms| (noise scale of F)          */
-  double ell[NPOS];/* pointwise log-likelihood (without log C(N,y))  */
+  double ell[NPOS];/* pointwise log-likelihood (without log C(N,y));
+                    * the full log-pmf in the polish phase             */
 } evalres;
+
+static long double lrise_l(long double n, long double s);
 
 /* absolute position |z| - 1 of dense column i */
 static int kpos(int i) { return i < NHALF ? i : i - NHALF; }
 
-/* Evaluate the objective at u for the points i in [lo, hi). */
+/* Evaluate the objective at u for the points i in [lo, hi).
+ *
+ * accf = 0: F = -(sum_i ell_i + ln p) with ell_i the beta-binomial log-pmf
+ * without the data-only log C(N,y), as a sum of six lnGamma values per point
+ * (each ~N ln N: at N ~ 1e7 the sum carries ~1e-6 of rounding).
+ * accf = 1 (the polish phase of fit_one): ell_i is the full log-pmf in the
+ * cancellation-free form R(y,a) + R(N-y,b) - R(N,phi) (bb_logpmf_full, below;
+ * F shifts by the constant sum log C(N,y)), so F resolves differences of
+ * ~1e-10 and the line search can follow a flat valley to its optimum.  The
+ * gradient and Hessian are the same in both forms. */
 static void evaluate(int model, const uint32_t* y, const uint32_t* N, int lo,
-                     int hi, const double u[4], evalres* r) {
+                     int hi, const double u[4], evalres* r, int accf) {
   double q = sigm(u[P_Q]);
   double omq = sigm(-u[P_Q]);
   double l1mq = -softplus(u[P_Q]); /* ln(1-q) */
@@ -190,7 +202,13 @@ static void evaluate(int model, const uint32_t* y, const uint32_t* N, int lo,
     double t1 = o_lgamma(yy + a), t2 = o_lgamma(NN - yy + b), t3 = o_lgamma(NN + phi);
     double t4 = o_lgamma(a), t5 = o_lgamma(b), t6 = o_lgamma(phi);
     double ell = (t1 - t4) + (t2 - t5) - (t3 - t6); /* exact 0 when N = 0 */
-    mag += fabs(t1) + fabs(t2) + fabs(t3) + fabs(t4) + fabs(t5) + fabs(t6);
+    if (accf) {
+      long double r1 = lrise_l(yy, a), r2 = lrise_l(NN - yy, b), r3 = lrise_l(NN, phi);
+      ell = (double)(r1 + r2 - r3);
+      mag += (double)(fabsl(r1) + fabsl(r2) + fabsl(r3));
+    } else {
+      mag += fabs(t1) + fabs(t2) + fabs(t3) + fabs(t4) + fabs(t5) + fabs(t6);
+    }
     r->ell[i] = ell;
     L += ell;
     double Pa = o_digamma(yy + a) - o_digamma(a);
@@ -453,6 +471,7 @@ typedef struct {
   evalres r;
   int evals;
   int status;
+  int polished; /* the fit entered the polish phase */
 } fitres;
 
 #include <stdio.h>
@@ -466,7 +485,8 @@ static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
   evalres cur, tr;
   if (u0) memcpy(u, u0, sizeof(u));
   else init_u(model, y, N, lo, hi, u);
-  evaluate(model, y, N, lo, hi, u, &cur);
+  int accf = 0; /* the polish phase (below): F in the cancellation-free form */
+  evaluate(model, y, N, lo, hi, u, &cur, accf);
   int evals = 1, status = MDFIT_MAXITER;
   if (!isfinite(cur.F)) {
     status = MDFIT_NONFINITE;
@@ -481,7 +501,7 @@ static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
   int nc = 0, n_nc = 0, st_exh = MDFIT_MAXITER; /* the saddle escape (below) */
   while (evals < max_iter) {
     for (int j = 0; j < 4; j++) ut[j] = clampd(u[j] + t * d[j], U_LO[j], U_HI[j]);
-    evaluate(model, y, N, lo, hi, ut, &tr);
+    evaluate(model, y, N, lo, hi, ut, &tr, accf);
     evals++;
     const double noise = NOISE_F * (cur.mag + fabs(cur.F));
     int acc = isfinite(tr.F) &&
@@ -510,6 +530,25 @@ static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
       }
     } else {
       t *= 0.5;
+      /* the polish phase: once the backtracking step's predicted decrease
+       * t |g.d| is below F's rounding scale (the sum of ~N ln N-sized lnGamma
+       * values), F can no longer judge the trials -- in a flat valley the
+       * stopping point would depend on the rounding path.  Once per fit:
+       * re-evaluate at u with F in the cancellation-free form (an evaluation;
+       * same g, H, hence the same d) and restart the line search at t = 1; the
+       * fit keeps that form to its end. */
+      if (!accf && evals < max_iter) {
+        double gd = 0;
+        for (int j = 0; j < 4; j++) gd += cur.g[j] * d[j];
+        if (t < 1e-12 || t * fabs(gd) <= noise) {
+          accf = 1;
+          evaluate(model, y, N, lo, hi, u, &cur, accf);
+          evals++;
+          indef = direction(model, u, cur.g, cur.H, d);
+          t = 1.0;
+          continue;
+        }
+      }
       if (t < 1e-12) { /* line search exhausted */
         /* the flat tail of log delta (phi -> 2): the Newton step heads down a
          * tail in which F changes below its rounding scale, so the stopping
@@ -534,7 +573,7 @@ static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
          * as the kernel does: it keeps no H), step along nc_direction from t = 1
          * halving to 1e-3, accepting only a decrease beyond F's rounding. */
         if (indef && n_nc < 4 && evals < max_iter) {
-          evaluate(model, y, N, lo, hi, u, &tr);
+          evaluate(model, y, N, lo, hi, u, &tr, accf);
           evals++;
           if (nc_direction(model, u, tr.g, tr.H, d)) {
             n_nc++;
@@ -553,6 +592,7 @@ done:
   out->r = cur;
   out->evals = evals;
   out->status = status;
+  out->polished = accf;
 }
 
 /* ---- pointwise log-likelihood at a mode (fits.py:126-133) -----------------
@@ -756,7 +796,7 @@ static void fit_taxon(const uint32_t* y, const uint32_t* N, const uint32_t* mm,
     dg[4] = f[s].r.F;
     dg[5] = f[s].evals;
     dg[6] = f[s].status;
-    dg[7] = 0.0;
+    dg[7] = f[s].polished;
   }
   double p[3];
   /* PMD-all: predictions + D_max (fits.py:249-261: median / HPDI at z = +1) */
@@ -855,7 +895,7 @@ void oracle_objective(int model, int subset, const uint32_t* y, const uint32_t* 
   int lo = subset == 2 ? NHALF : 0, hi = subset == 1 ? NHALF : NPOS;
   evalres r;
   memset(&r, 0, sizeof(r));
-  evaluate(model, y, N, lo, hi, u, &r);
+  evaluate(model, y, N, lo, hi, u, &r, 0);
   *F = r.F;
   for (int j = 0; j < 4; j++) {
     g4[j] = r.g[j];

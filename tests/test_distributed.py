@@ -112,3 +112,49 @@ def test_record_views_layout(n):
     rec.out.copy_(torch.arange(n * 80, dtype=torch.float64).view(n, 80))
     rec.stage()
     np.testing.assert_array_equal(rec.res.numpy(), rec.out[:, :NRES_GATHER].numpy())
+
+
+def _failing_worker(rank, world, port, q):
+    """The `metadamage fit` wrapper (distributed.run_distributed) where rank 1
+    raises before the collective rank 0 is about to enter."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    from metadamage_amd.distributed import all_ranks_agree, init_from_env, run_distributed
+
+    init_from_env_gloo = lambda: init_from_env("gloo")  # noqa: E731
+
+    def body():
+        if rank == 1:
+            raise RuntimeError("bad input file on rank 1")
+        return all_ranks_agree(True)  # rank 0 waits here for its peer
+
+    import metadamage_amd.distributed as d
+
+    d.init_from_env = init_from_env_gloo  # CPU test: gloo instead of RCCL
+    try:
+        run_distributed(body)
+        q.put((rank, "ok"))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, type(e).__name__))
+
+
+def test_a_failing_rank_does_not_hang_the_job():
+    """a rank that raises leaves the group without a barrier, so
+    the healthy rank's pending collective fails instead of pairing with it and
+    hanging; both processes exit promptly."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_failing_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=90)
+    alive = [p.is_alive() for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert not any(alive), "a rank is still waiting in a collective"
+    got = dict(q.get(timeout=5) for _ in range(2))
+    assert got[1] == "RuntimeError"
+    assert got[0] != "ok"  # the healthy rank's collective failed (peer gone) rather than completing

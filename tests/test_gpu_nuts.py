@@ -19,7 +19,7 @@ def nuts_engine():
     import torch
 
     if not torch.cuda.is_available():
-        pytest.skip("no GPU")
+        pytest.fail("gpu test selected but no HIP device is visible")
     from metadamage_amd import engine
 
     return engine

@@ -44,8 +44,9 @@ def test_oracle_subfit_optimum_is_local_min(oracle_lib, subset):
     names, y, N = _batch()
     rng = np.random.default_rng(subset)
     for i in range(len(names)):
-        u, F, ev, st = oracle_lib.fit_subfit(0, subset, y[i, :30], N[i, :30])
+        u, _, ev, st = oracle_lib.fit_subfit(0, subset, y[i, :30], N[i, :30])
         assert st == 0, (names[i], subset)
+        F = oracle_lib.objective(0, subset, y[i, :30], N[i, :30], u)[0]  # the lnGamma-sum form
         noise = 1e-12 * abs(F) + 1e-9
         for j in range(4):
             for h in (1e-4, -1e-4, 1e-6, -1e-6):
@@ -70,9 +71,12 @@ def test_oracle_escapes_a_saddle(oracle_lib):
     u0 = np.array(sd["u"])
     F0, g0, H0, _ = oracle_lib.objective(sd["model"], sd["subset"], y, N, u0)
     assert np.linalg.eigvalsh(H0)[0] < 0  # indefinite: a saddle, not a minimum
-    u1, F1, ev1, st1 = oracle_lib.fit_subfit(sd["model"], sd["subset"], y, N, u0=u0)
-    u2, F2, ev2, st2 = oracle_lib.fit_subfit(sd["model"], sd["subset"], y, N)
+    u1, _, ev1, st1 = oracle_lib.fit_subfit(sd["model"], sd["subset"], y, N, u0=u0)
+    u2, _, ev2, st2 = oracle_lib.fit_subfit(sd["model"], sd["subset"], y, N)
     assert st1 == 0 and st2 == 0
+    # F in one form at both modes (a fit that polished reports the other form)
+    F1 = oracle_lib.objective(sd["model"], sd["subset"], y, N, u1)[0]
+    F2 = oracle_lib.objective(sd["model"], sd["subset"], y, N, u2)[0]
     assert F1 < F0 - 1e-2  # escaped (the saddle is ~0.022 above the optimum)
     assert abs(F1 - F2) <= 1e-9 * abs(F2)
     assert np.abs(u1 - u2).max() < 1e-5, (u1, u2)
@@ -90,22 +94,11 @@ def test_kernel_converges_at_bounds_like_the_oracle(oracle_lib):
     out, pred, st = engine.fit_batch(y, N)
     ref, rpred, rst = oracle_lib.fit_batch(y, N)
     assert (st == 0).all() and (rst == 0).all(), (st, rst)
-    kinds = [(0, 0), (1, 0), (0, 1), (0, 2), (1, 1), (1, 2)]  # (model, subset) of the 6 sub-fits
-    for i, name in enumerate(names):
-        rel = mixed_rel(out[i, :25], ref[i, :25]).max()
-        if rel < RTOL:
-            continue
-        # a flat valley (c5_102058064: q moves 7.7e-4 while F changes below its
-        # rounding scale; the five m1_* taxa of the 1M-taxon
-        # parity run, up to 1.45e-3 on q_mean for m1_t839013): then
-        # the GPU's modes must be optimal to F's resolution -- the oracle's
-        # objective at them within its own optimum's rounding scale -- for
-        # every sub-fit
-        for s, (model, subset) in enumerate(kinds):
-            q, A, c, phi = out[i, 32 + 8 * s: 36 + 8 * s]
-            u = np.array([np.log(q / (1 - q)), np.log(A / (1 - A)) if model == 0 else 0.0,
-                          c if model == 0 else 0.0, np.log(phi - 2.0)])
-            Fg = oracle_lib.objective(model, subset, y[i, :30], N[i, :30], u)[0]
-            Fo = ref[i, 32 + 8 * s + 4]
-            assert Fg <= Fo + 1.4e-14 * 1e3 * abs(Fo) + 1e-9, (name, s, Fg - Fo)
-        assert rel < 2e-3, (name, rel)
+    rel = mixed_rel(out[:, :25], ref[:, :25])
+    worst = rel.max(1)
+    # the polish phase makes the flat-valley modes independent of
+    # the rounding path: every case, the five m1_* and c5_102058064 included,
+    # meets the 1e-4 bar
+    assert (worst < RTOL).all(), dict(zip(names, worst))
+    # the same sub-fits polished on both sides
+    assert (out[:, 32 + 7::8][:, :6] == ref[:, 32 + 7::8][:, :6]).all()

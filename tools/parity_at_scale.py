@@ -64,6 +64,10 @@ def main() -> None:
         line.update(config=label, n_taxa=T, seed=seed, gpu_status_ok=float((st == 0).mean()),
                     cpu_status_ok=float((rst == 0).mean()),
                     status_mismatch_tax_index=[int(i) for i in np.nonzero(st != rst)[0][:10]],
+                    not_ok=[[int(i), int(st[i]), int(rst[i])] for i in np.nonzero((st != 0) | (rst != 0))[0][:20]],
+                    polished_subfits=int(out[:, 32 + 7::8][:, :6].sum()),
+                    polished_subfits_oracle=int(ref[:, 32 + 7::8][:, :6].sum()),
+                    polish_mismatch=int((out[:, 32 + 7::8][:, :6] != ref[:, 32 + 7::8][:, :6]).sum()),
                     pred_max_abs=float(np.nanmax(np.abs(pred - rpred))), oracle_s=round(cpu_s, 2),
                     oracle_threads=threads)
         print(json.dumps(line), flush=True)
