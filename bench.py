@@ -52,6 +52,7 @@ sys.path.insert(0, str(ROOT))
 TAXA_PER_GPU = 10_000
 C4_TAXA = 1_000_000
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+NODE_GPUS = 8  # one MI355X node
 # bytes per taxon:
 #  algorithmic: y,N 2x30x4 in + 26 numeric result fields x8 out
 #  fit_kernel as built: y,N 2x30x4 + 6 initial points 6x4x8 in, 6 sub-fit records 6x8x8 out
@@ -150,7 +151,7 @@ def host_cores() -> tuple[int, int]:
     return (min(visible, share) if share > 0 else visible), (os.cpu_count() or visible)
 
 
-def ref_dispatch_baseline(cores: int, taxa: int = 500) -> dict | None:
+def ref_dispatch_baseline(cores: int, taxa: int = 1000) -> dict | None:
     """tools/cpu_reference_dispatch.py in a child process, started before this
     process touches the GPU (its Pool forks workers)."""
     import subprocess
@@ -247,6 +248,29 @@ def main():
     call_ms_sum = elapsed * 1e3 / args.steps * n_calls  # the step by the wall clock
     engine.profile_enable(False)
     assert n_calls == min(args.steps, 256), (n_calls, args.steps)  # the library keeps up to 256 calls
+    ranks = None
+    if world > 1:
+        # per-rank split of a step (after the timed region, so its
+        # synchronisations stay out of it): the fit call and the gather, by
+        # the wall clock over a few extra steps; every rank's pair to rank 0
+        nb = max(2, min(args.steps, 5))
+        fit_s = gat_s = 0.0
+        for _ in range(nb):
+            dist.barrier()
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            engine.fit_batch_device(ty, tN, tm, opts, fb, stream=stream)
+            torch.cuda.synchronize(dev)
+            t2 = time.perf_counter()
+            gather_records(rec.stage(), cap, rank, world)
+            torch.cuda.synchronize(dev)
+            fit_s += t2 - t1
+            gat_s += time.perf_counter() - t2
+        mine = torch.tensor([fit_s / nb * 1e3, gat_s / nb * 1e3, float(T)], dtype=torch.float64, device=red_dev)
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        ranks = [{"rank": r, "taxa": int(v[2].item()), "fit_ms": round(float(v[0].item()), 3),
+                  "gather_ms": round(float(v[1].item()), 3)} for r, v in enumerate(allr)]
 
     o = fb.out.cpu().numpy()
     st = fb.status.cpu().numpy()
@@ -357,7 +381,14 @@ def main():
         }
         if world == 1:
             line["host_to_host"] = host_to_host(engine, b, opts, dev, max(5, args.steps // 2))
-        if world == 1 and workload == "c2" and not args.no_c4_base:
+        if ranks is not None:
+            line["per_rank"] = ranks
+            line["per_rank_note"] = ("a step split into the fit call and the one gather by the wall clock, "
+                                     "measured after the timed region (synchronised per phase)")
+        if (world == 1 and workload == "c2" or workload == "c4" and world > 1) and not args.no_c4_base:
+            # the strong-scaling base, measured in the same run on rank 0's GPU
+            # (at N > 1 the other ranks wait at the closing barrier):
+            # value_N / (N * c4_one_gpu.value) is the C4 scaling efficiency
             line["c4_one_gpu"] = c4_one_gpu(engine, _lib, generate, dev, stream)
         if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure
             line["cpu_baseline"], ref = cpu_baseline(b, cores, visible)
@@ -587,6 +618,17 @@ def cpu_baseline(b, cores: int, visible: int):
         f"({dt:.2f} s; min {min(times):.2f}, max {max(times):.2f}); 1-thread rate on the first {n1}: "
         f"{n1 / d1:.1f} fits/s",
         "single_thread_value": round(n1 / d1, 1),
+        "node_estimate": {
+            "value": round(b.n_taxa / dt * NODE_GPUS * 16 / cores, 1),
+            "cores": NODE_GPUS * 16,
+            "kind": "extrapolated",
+            "note": f"the node's CPU share beside an {NODE_GPUS}-GPU line ({NODE_GPUS} x the 16-thread share per "
+            "GPU), scaled linearly from the measured rate on this rank's share (the taxa are independent, the "
+            f"measured {cores}-thread parallel efficiency vs 1 thread is "
+            f"{b.n_taxa / dt / (cores * n1 / d1):.2f}); not run at that width: a one-GPU box grants "
+            "16 threads of its host (OMP_NUM_THREADS), running the oracle on all visible CPUs would take "
+            "other jobs' cores",
+        },
         "note": "cores = the process's CPU share (affinity / OMP_NUM_THREADS: 16 per GPU on the box)",
     }, ref
 

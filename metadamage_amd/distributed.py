@@ -191,11 +191,26 @@ def run_distributed(fn, *args, **kwargs):
 def unpack_gathered(parts, n_taxa: int, world: int):
     """Concatenate gathered shards back into df_counts order (host numpy);
     the parts may be device (RCCL) or host (gloo) buffers."""
+    import torch
+
     outs, preds, sts = [], [], []
+    if parts and parts[0].is_cuda:
+        # every part's D2H copy queued at once into one pinned host buffer,
+        # then one synchronisation (not a blocking copy per part)
+        n = sum(p.numel() for p in parts)
+        host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        off = []
+        o0 = 0
+        for p in parts:
+            host[o0 : o0 + p.numel()].copy_(p, non_blocking=True)
+            off.append(o0)
+            o0 += p.numel()
+        torch.cuda.current_stream(parts[0].device).synchronize()
+        parts = [host[o : o + p.numel()] for o, p in zip(off, parts)]
     for r, part in enumerate(parts):
         lo, hi = shard_range(n_taxa, r, world)
         n_cap = part.numel() // REC_BYTES
-        p, s, o = packed_views(part.cpu(), n_cap)  # one D2H copy per part
+        p, s, o = packed_views(part, n_cap)
         outs.append(o[: hi - lo].numpy())
         preds.append(p[: hi - lo].numpy())
         sts.append(s[: hi - lo].numpy())
