@@ -70,6 +70,8 @@ __device__ __forceinline__ unsigned long long stamp() {
 }
 #endif
 
+constexpr int kHpdiCtr = 16;  // workspace ints: [16] front-list count, [17] claim counter, [18] back-list count (zeroed by K0)
+
 // ---------------------------------------------------------------------------
 // K0: initial points (oracle: init_u)
 // ---------------------------------------------------------------------------
@@ -81,11 +83,12 @@ __device__ __forceinline__ int kpos(int i) { return i < kNHalf ? i : i - kNHalf;
 // by its own mode when it converged -- the warm start).
 __global__ __launch_bounds__(256) void init_kernel(const uint32_t* __restrict__ gy,
                                                    const uint32_t* __restrict__ gN, int64_t T,
-                                                   double* __restrict__ out, int* __restrict__ ws) {
+                                                   double* __restrict__ out, int* __restrict__ ws, int keep_hpdi) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   // the fit kernel's queue counters (workspace, 256 B): zeroed here instead of
   // by a separate memset launch (stream order puts this before the fit kernel)
-  if (i < 64) ws[i] = 0;
+  // (keep_hpdi: the MDFIT_EXP_OVERLAP timing experiment keeps the HPDI list)
+  if (i < 64 && !(keep_hpdi && i >= kHpdiCtr && i < kHpdiCtr + 3)) ws[i] = 0;
   if (i >= MDFIT_NSUBFIT * T) return;
   const int64_t taxon = i / MDFIT_NSUBFIT;
   const int sub = (int)(i % MDFIT_NSUBFIT);  // 0 PMD-all 1 null-all 2 PMD-f 3 PMD-r 4 null-f 5 null-r
@@ -169,7 +172,6 @@ constexpr unsigned kEscIndef = 1u, kEscProbe = 2u, kEscNc = 4u, kEscExhOk = 8u, 
 // The predictive HPDI's per-position step (K4a, and the fused prep of the PPL-1
 // fit kernel): shared definitions
 // ---------------------------------------------------------------------------
-constexpr int kHpdiCtr = 16;  // workspace ints: [16] front-list count, [17] claim counter, [18] back-list count (zeroed by K0)
 
 struct HpdiIO {
   // kFit
@@ -524,15 +526,17 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         }
       } else {
         t *= 0.5;
-        if (!(esc & kEscPolish) && evals < max_iter &&
-            (t < 1e-12 || t * fabs(curGd) <= kNoiseF * (curMag + fabs(curF)))) {
+        const bool unresolved = t * fabs(curGd) <= kNoiseF * (curMag + fabs(curF));
+        if (!(esc & kEscPolish) && evals < max_iter && (t < 1e-12 || unresolved)) {
           // the polish phase (oracle: fit_one): the backtracking step's
           // predicted decrease is below F's rounding -- re-evaluate at u with F
           // in the cancellation-free form next trip, then restart at t = 1
           esc |= kEscPolish | kEscPolishProbe;
           d[0] = d[1] = d[2] = d[3] = 0.0;
           t = 1.0;
-        } else if (t < 1e-12) {  // line search exhausted (oracle: fit_one)
+        } else if (t < 1e-12 || ((esc & kEscPolish) && unresolved)) {
+          // line search exhausted (oracle: fit_one), in the polish phase also
+          // when even the cancellation-free F cannot resolve the decrease
           if (!(esc & kEscRescued) && u[3] < 0.0 && d[3] < 0.0 && u[3] > kULo[3]) {
             // the flat tail of log delta: jump onto its lower bound once
             esc |= kEscRescued | kEscRelax;
@@ -1100,6 +1104,12 @@ void prof_record(int slot, hipStream_t s) {
 }  // namespace
 
 namespace {
+// development A/B knobs (environment; unset = the product configuration)
+int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+
 // MAP workspace: 256 B of counters, the PMD-all (q, A, c, phi) of every taxon
 // (K3a -> K4; n_theta = n_taxa, 0 for the array entry point), then the HPDI
 // wide-window records
@@ -1182,7 +1192,7 @@ int launch_hpdi(const mdfit::HpdiIO& io, int64_t n_items, int* ctr, mdfit::hpdi:
   }
   // no more waves than are resident, and no more than the items need (the
   // kernel strides over the wide list, whose length only the device knows)
-  const int64_t g = fit_grid(mdfit::hpdi_wide_kernel<kFit>, n_items, mdfit::kWave);
+  const int64_t g = fit_grid(mdfit::hpdi_wide_kernel<kFit>, n_items, mdfit::kWave, env_int("MDFIT_HPDI_WAVES_PER_CU", 0));
   hipLaunchKernelGGL(mdfit::hpdi_wide_kernel<kFit>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, io, n_items, ctr,
                      recs);
   return check_launch("hpdi_wide_kernel");
@@ -1276,8 +1286,26 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
     return 0;
   }
   const int64_t n_init = MDFIT_NSUBFIT * n_taxa;
+  // MDFIT_EXP_OVERLAP=1 (timing experiment only, results of the HPDI columns
+  // meaningless): K4b runs on the side stream beside the fit kernel, draining
+  // the wide-window list the PREVIOUS call of the same batch left in the
+  // workspace, while the fit kernel skips its fused HPDI step -- the call time
+  // a fit/HPDI overlap could reach at PPL 1
+  const bool exp_overlap = env_int("MDFIT_EXP_OVERLAP", 0) == 1 && n_taxa < kPpl2MinTaxa;
+  mdfit::hpdi::WideRec* recs0 = hpdi_recs(workspace, n_taxa);
+  if (exp_overlap && hipMemsetAsync(ws + mdfit::kHpdiCtr + 1, 0, 4, s) != hipSuccess)
+    return set_err(MDFIT_E_HIP, "memset");
+  ForkScope fork0(exp_overlap ? side_fork() : nullptr, s);
+  if (exp_overlap) {
+    mdfit::HpdiIO io{};
+    io.gN = N;
+    io.out = out;
+    io.pred = pred;
+    io.per = pred != nullptr ? mdfit::kNPos : 1;
+    if (int rc = launch_hpdi<true>(io, n_taxa * io.per, ws + mdfit::kHpdiCtr, recs0, fork0.side(), false)) return rc;
+  }
   hipLaunchKernelGGL(mdfit::init_kernel, dim3((unsigned)((n_init + 255) / 256)), dim3(256), 0, s, y, N,
-                     n_taxa, out, ws);
+                     n_taxa, out, ws, exp_overlap ? 1 : 0);
   if (int rc = check_launch("init_kernel")) return rc;
   // lane layout of the fit kernel (bitwise-identical results): 2 points per
   // lane for batches that fill the chip several times over, 1 below (lower
@@ -1289,14 +1317,14 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   mdfit::hpdi::WideRec* recs = hpdi_recs(workspace, n_taxa);
   int* hctr = ws + mdfit::kHpdiCtr;
   if (ppl == 2) {
-    const int64_t g = fit_grid(mdfit::fit_kernel<2>, 2 * n_taxa, 4);
+    const int64_t g = fit_grid(mdfit::fit_kernel<2>, 2 * n_taxa, 4, env_int("MDFIT_FIT_WAVES_PER_CU", 0));
     hipLaunchKernelGGL(mdfit::fit_kernel<2>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, y, N, n_taxa,
                        o.max_iter, o.tol_step, out, ws, pred, per, hctr, (mdfit::hpdi::WideRec*)nullptr);
   } else {
     // PPL 1 also runs the HPDI's per-position step (K4a) as each PMD-all fit ends
-    const int64_t g = fit_grid(mdfit::fit_kernel<1>, 2 * n_taxa, 2);
+    const int64_t g = fit_grid(mdfit::fit_kernel<1>, 2 * n_taxa, 2, env_int("MDFIT_FIT_WAVES_PER_CU", 0));
     hipLaunchKernelGGL(mdfit::fit_kernel<1>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, y, N, n_taxa,
-                       o.max_iter, o.tol_step, out, ws, pred, per, hctr, recs);
+                       o.max_iter, o.tol_step, out, ws, pred, per, hctr, exp_overlap ? nullptr : recs);
   }
   if (int rc = check_launch("fit_kernel")) return rc;
   prof_record(2, s);
@@ -1309,7 +1337,7 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
                        out, theta);
     if (int rc = check_launch("theta_kernel")) return rc;
   }
-  ForkScope fork(side_fork(), s);
+  ForkScope fork(exp_overlap ? nullptr : side_fork(), s);
   hipStream_t sa = fork.side();
   hipLaunchKernelGGL(mdfit::assemble_kernel, dim3((unsigned)n_taxa), dim3(mdfit::kWave), 0, sa, y, N,
                      mm, n_taxa, out, pred, status);
@@ -1321,9 +1349,11 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
     io.out = out;
     io.pred = pred;
     io.per = per;
-    if (int rc = launch_hpdi<true>(io, n_taxa * io.per, hctr, recs, s, ppl == 2)) return rc;
+    if (!exp_overlap)
+      if (int rc = launch_hpdi<true>(io, n_taxa * io.per, hctr, recs, s, ppl == 2)) return rc;
   }
   if (int rc = fork.join()) return rc;
+  if (int rc = fork0.join()) return rc;
   prof_record(3, s);
   if (g_prof.on && g_prof.n < kProfMax) ++g_prof.n;
   return 0;

@@ -27,14 +27,16 @@ void prof_mark(int slot, hipStream_t s);
 // persistent grid: no more waves than can be resident at once (so every
 // wave starts immediately and pulls work until its queue is drained), a
 // multiple of the 8 queues
+// (cap_per_cu > 0: at most that many waves per CU -- development A/B)
 template <typename K>
-int64_t fit_grid(K kernel, int64_t ntask, int fits_per_wave) {
+int64_t fit_grid(K kernel, int64_t ntask, int fits_per_wave, int cap_per_cu = 0) {
   int dev = 0, n_cu = 256, per_cu = 8;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
     n_cu = 256;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kWave, 0) != hipSuccess || per_cu <= 0)
     per_cu = 8;
+  if (cap_per_cu > 0 && cap_per_cu < per_cu) per_cu = cap_per_cu;
   const int64_t want = (ntask + fits_per_wave - 1) / fits_per_wave;
   const int64_t cap = (int64_t)n_cu * per_cu;
   int64_t g = want < cap ? want : cap;

@@ -503,6 +503,7 @@ static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
     for (int j = 0; j < 4; j++) ut[j] = clampd(u[j] + t * d[j], U_LO[j], U_HI[j]);
     evaluate(model, y, N, lo, hi, ut, &tr, accf);
     evals++;
+    /* (in the polish phase mag is the sum of the |R| terms of the cancellation-free form) */
     const double noise = NOISE_F * (cur.mag + fabs(cur.F));
     int acc = isfinite(tr.F) &&
               (nc ? tr.F < cur.F - noise
@@ -537,19 +538,22 @@ static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
        * re-evaluate at u with F in the cancellation-free form (an evaluation;
        * same g, H, hence the same d) and restart the line search at t = 1; the
        * fit keeps that form to its end. */
-      if (!accf && evals < max_iter) {
-        double gd = 0;
-        for (int j = 0; j < 4; j++) gd += cur.g[j] * d[j];
-        if (t < 1e-12 || t * fabs(gd) <= noise) {
-          accf = 1;
-          evaluate(model, y, N, lo, hi, u, &cur, accf);
-          evals++;
-          indef = direction(model, u, cur.g, cur.H, d);
-          t = 1.0;
-          continue;
-        }
+      double gdc = 0;
+      for (int j = 0; j < 4; j++) gdc += cur.g[j] * d[j];
+      const int unresolved = t * fabs(gdc) <= noise;
+      if (!accf && evals < max_iter && (t < 1e-12 || unresolved)) {
+        accf = 1;
+        evaluate(model, y, N, lo, hi, u, &cur, accf);
+        evals++;
+        indef = direction(model, u, cur.g, cur.H, d);
+        t = 1.0;
+        continue;
       }
-      if (t < 1e-12) { /* line search exhausted */
+      /* exhausted: t below 1e-12, or (polish phase) the predicted decrease
+       * below even the cancellation-free F's rounding -- where noise-level
+       * "decreases" would otherwise be accepted at ever smaller steps (a saddle
+       * whose shifted Newton step is ~0 then never exhausts the search) */
+      if (t < 1e-12 || (accf && unresolved)) { /* line search exhausted */
         /* the flat tail of log delta (phi -> 2): the Newton step heads down a
          * tail in which F changes below its rounding scale, so the stopping
          * point would depend on the rounding path.  Once per fit: jump log delta
