@@ -9,6 +9,7 @@ which the installed pyarrow rejects; we write "2.6".
 
 from __future__ import annotations
 
+import ctypes
 import json
 import os
 import threading
@@ -20,6 +21,50 @@ import pyarrow.parquet as pq
 from . import utils
 
 PARQUET_VERSION = "2.6"
+PQ_LIB = Path(__file__).resolve().parent / "libmdpq.so"
+_PQ = None
+
+
+def _native_writer():
+    """libmdpq.so (csrc/pqwrite.cpp): the same file as pq.write_table with the
+    columns of each row group encoded in parallel on Arrow's CPU pool.  Two
+    handles on the library: mdpq_unwrap through PyDLL (it touches the pyarrow
+    object, GIL held), mdpq_write through CDLL (GIL released while encoding, so
+    main()'s writer threads and the reader thread run beside it).  None when
+    the library is not built (pq.write_table then writes the same file on one
+    core)."""
+    global _PQ
+    if _PQ is None:
+        if not PQ_LIB.exists():
+            _PQ = False
+        else:
+            py, c = ctypes.PyDLL(str(PQ_LIB)), ctypes.CDLL(str(PQ_LIB))
+            py.mdpq_unwrap.argtypes = [ctypes.py_object]
+            py.mdpq_unwrap.restype = ctypes.c_void_p
+            c.mdpq_write.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                                     ctypes.c_int64]
+            c.mdpq_write.restype = ctypes.c_int
+            c.mdpq_last_error.restype = ctypes.c_char_p
+            py.mdpq_last_error.restype = ctypes.c_char_p
+            _PQ = (py, c)
+    return _PQ or None
+
+
+def write_table(table: "pa.Table", path, dict_cols) -> None:
+    """pq.write_table(table, path, version="2.6", use_dictionary=dict_cols,
+    write_statistics=dict_cols) -- natively when libmdpq.so is built."""
+    nat = _native_writer()
+    if nat is None:
+        pq.write_table(table, path, version=PARQUET_VERSION, use_dictionary=list(dict_cols) or False,
+                       write_statistics=list(dict_cols) or False)
+        return
+    py, c = nat
+    h = py.mdpq_unwrap(table)
+    if not h:
+        raise RuntimeError(f"mdpq_unwrap: {py.mdpq_last_error().decode()}")
+    names = (ctypes.c_char_p * max(1, len(dict_cols)))(*[n.encode() for n in dict_cols])
+    if c.mdpq_write(h, os.fsencode(str(path)), names, len(dict_cols), 0) != 0:
+        raise OSError(f"{path}: {c.mdpq_last_error().decode()}")
 
 
 class Parquet:
@@ -73,8 +118,7 @@ class Parquet:
         # file or a complete one, never a half-written parquet
         tmp = self.filename.with_name(f".{self.filename.name}.{os.getpid()}.{threading.get_ident()}.tmp")
         try:
-            pq.write_table(table, tmp, version=PARQUET_VERSION, use_dictionary=cats,
-                           write_statistics=cats or False)
+            write_table(table, tmp, cats)
             os.replace(tmp, self.filename)
         finally:
             if tmp.exists():
