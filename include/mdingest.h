@@ -99,6 +99,18 @@ int mdi_gather(int64_t rows, const int64_t* perm, int64_t n_keep, const int64_t*
  * n_threads <= 0: hardware concurrency. */
 int mdi_noise(const uint32_t* mm, int64_t n_taxa, int n_threads, double* out3);
 
+/* mdi_codes / mdi_remap: the categorical columns of the kept rows
+ * (astype("category") of tax_id, tax_name, tax_rank, strand; utils.py:329-356)
+ * without a per-row pass in Python.  mdi_codes, for each of n_cols int32 code
+ * columns in[c][rows]: out[c][i] = in[c][perm[i]] (i < n_keep) and used[c][k]
+ * = 1 where code k (< n_table[c]) occurs among them (used zeroed here).  The
+ * caller orders the used values (the sorted categories) and mdi_remap then
+ * rewrites every code in place: codes[c][i] = remap[c][codes[c][i]].  Both
+ * parallel over row ranges; n_threads <= 0: hardware concurrency. */
+int mdi_codes(int64_t n_keep, const int64_t* perm, int n_cols, const int32_t* const* in, const int32_t* n_table,
+              int n_threads, int32_t* const* out, uint8_t* const* used);
+int mdi_remap(int64_t n, int n_cols, int32_t* const* codes, const int32_t* const* remap, int n_threads);
+
 /* message of the last failed mdi_select / mdi_gather on this thread */
 const char* mdi_counts_error(void);
 

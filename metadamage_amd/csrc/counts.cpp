@@ -222,6 +222,85 @@ const char* mdi_counts_error(void) { return g_cerr; }
 
 }  // extern "C"
 
+namespace {
+int pool_size(int n_threads, int64_t n) {
+  int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+  if (nt < 1) nt = 1;
+  if (n < (int64_t)nt * 65536) nt = (int)std::max<int64_t>(1, n / 65536);
+  return nt > 64 ? 64 : nt;
+}
+
+template <typename F>
+void for_ranges(int nt, int64_t n, F f) {
+  if (nt <= 1) {
+    f(0, (int64_t)0, n);
+    return;
+  }
+  std::vector<std::thread> pool;
+  for (int i = 0; i < nt; ++i) pool.emplace_back(f, i, n * i / nt, n * (i + 1) / nt);
+  for (auto& t : pool) t.join();
+}
+}  // namespace
+
+extern "C" {
+
+int mdi_codes(int64_t n_keep, const int64_t* perm, int n_cols, const int32_t* const* in, const int32_t* n_table,
+              int n_threads, int32_t* const* out, uint8_t* const* used) {
+  if (n_keep < 0 || n_cols < 0 || n_cols > 8 || (n_cols > 0 && (!in || !n_table || !out || !used)) ||
+      (n_keep > 0 && !perm))
+    return arg_error("mdi_codes: bad arguments");
+  for (int c = 0; c < n_cols; ++c) {
+    if (n_table[c] < 0 || !in[c] || !out[c] || !used[c]) return arg_error("mdi_codes: bad column");
+    std::memset(used[c], 0, (size_t)n_table[c]);
+  }
+  const int nt = pool_size(n_threads, n_keep);
+  // per-thread usage flags, OR-merged (the tables are per taxon at most: small)
+  std::vector<std::vector<uint8_t>> seen((size_t)nt * (size_t)n_cols);
+  std::vector<uint8_t> bad((size_t)nt, 0);
+  for_ranges(nt, n_keep, [&](int tid, int64_t lo, int64_t hi) {
+    for (int c = 0; c < n_cols; ++c) {
+      std::vector<uint8_t>& u = seen[(size_t)tid * n_cols + c];
+      u.assign((size_t)n_table[c], 0);
+      const int32_t* src = in[c];
+      int32_t* dst = out[c];
+      const int32_t m = n_table[c];
+      for (int64_t i = lo; i < hi; ++i) {
+        const int32_t k = src[perm[i]];
+        if (k < 0 || k >= m) {
+          bad[tid] = 1;
+          continue;
+        }
+        dst[i] = k;
+        u[(size_t)k] = 1;
+      }
+    }
+  });
+  for (int i = 0; i < nt; ++i)
+    if (bad[i]) return arg_error("mdi_codes: code out of its table");
+  for (int c = 0; c < n_cols; ++c)
+    for (int i = 0; i < nt; ++i) {
+      const std::vector<uint8_t>& u = seen[(size_t)i * n_cols + c];
+      for (size_t k = 0; k < u.size(); ++k) used[c][k] |= u[k];
+    }
+  return 0;
+}
+
+int mdi_remap(int64_t n, int n_cols, int32_t* const* codes, const int32_t* const* remap, int n_threads) {
+  if (n < 0 || n_cols < 0 || (n_cols > 0 && (!codes || !remap))) return arg_error("mdi_remap: bad arguments");
+  for (int c = 0; c < n_cols; ++c)
+    if (!codes[c] || !remap[c]) return arg_error("mdi_remap: bad column");
+  for_ranges(pool_size(n_threads, n), n, [&](int, int64_t lo, int64_t hi) {
+    for (int c = 0; c < n_cols; ++c) {
+      int32_t* x = codes[c];
+      const int32_t* m = remap[c];
+      for (int64_t i = lo; i < hi; ++i) x[i] = m[x[i]];
+    }
+  });
+  return 0;
+}
+
+}  // extern "C"
+
 // ---------------------------------------------------------------------------
 // mdi_noise: fits.py:359-376 per packed taxon (the oracle's noise() is the check)
 // ---------------------------------------------------------------------------

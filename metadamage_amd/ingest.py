@@ -58,6 +58,10 @@ def _load():
                                    ctypes.c_char_p, vp, ctypes.c_int, vp, vp, vp, vp, vp, vp]
         lib.mdi_gather.restype = ctypes.c_int
         lib.mdi_counts_error.restype = ctypes.c_char_p
+        lib.mdi_codes.argtypes = [i64, vp, ctypes.c_int, vp, vp, ctypes.c_int, vp, vp]
+        lib.mdi_codes.restype = ctypes.c_int
+        lib.mdi_remap.argtypes = [i64, ctypes.c_int, vp, vp, ctypes.c_int]
+        lib.mdi_remap.restype = ctypes.c_int
         lib.mdi_noise.argtypes = [vp, i64, ctypes.c_int, vp]
         lib.mdi_noise.restype = ctypes.c_int
         _LIB = lib
@@ -143,6 +147,41 @@ def _categorical_from_codes(codes: np.ndarray, table: np.ndarray) -> pd.Categori
     return pd.Categorical.from_codes(remap[codes], vals[order])
 
 
+def _ptrs(arrays, ctype):
+    return (ctype * len(arrays))(*[a.ctypes.data for a in arrays])
+
+
+def _categoricals(perm: np.ndarray, columns, n_threads: int = 0) -> list:
+    """[astype("category") of table[codes[perm]] for (codes, table) in columns]
+    (categories = the sorted distinct values present) with the per-row passes
+    -- gather through perm, usage, the remap to category order -- in the native
+    library, parallel over row ranges (mdi_codes / mdi_remap); only the used
+    values are sorted here."""
+    lib = _load()
+    k = len(perm)
+    ins = [np.ascontiguousarray(c, dtype=np.int32) for c, _ in columns]
+    sizes = np.array([len(tbl) for _, tbl in columns], np.int32)
+    outs = [np.empty(k, np.int32) for _ in columns]
+    used = [np.empty(max(1, len(tbl)), np.uint8) for _, tbl in columns]
+    perm = np.ascontiguousarray(perm, dtype=np.int64)
+    if lib.mdi_codes(k, perm.ctypes.data, len(columns), _ptrs(ins, ctypes.c_void_p), sizes.ctypes.data,
+                     int(n_threads), _ptrs(outs, ctypes.c_void_p), _ptrs(used, ctypes.c_void_p)) != 0:
+        raise ValueError(lib.mdi_counts_error().decode())
+    remaps, cats = [], []
+    for (_, tbl), u in zip(columns, used):
+        idx = np.flatnonzero(u[: len(tbl)])
+        vals = tbl[idx]
+        order = np.argsort(vals.astype(str) if vals.dtype == object else vals, kind="stable")
+        remap = np.zeros(max(1, len(tbl)), np.int32)
+        remap[idx[order]] = np.arange(len(idx), dtype=np.int32)
+        remaps.append(remap)
+        cats.append(vals[order])
+    if lib.mdi_remap(k, len(columns), _ptrs(outs, ctypes.c_void_p), _ptrs(remaps, ctypes.c_void_p),
+                     int(n_threads)) != 0:
+        raise ValueError(lib.mdi_counts_error().decode())
+    return [pd.Categorical.from_codes(o, dtype=pd.CategoricalDtype(c), validate=False) for o, c in zip(outs, cats)]
+
+
 def _const_category(value, n: int) -> pd.Categorical:
     """astype("category") of a column holding one value (no categories when empty)."""
     return pd.Categorical.from_codes(np.zeros(n, np.int32), np.array([value] if n else [], object))
@@ -209,17 +248,19 @@ def compute_counts(cfg, table: Table | None = None, n_threads: int = 0) -> pd.Da
                         f2.ctypes.data, ys.ctypes.data)
     if rc != 0:
         raise AssertionError(lib.mdi_counts_error().decode())
-    tax = taxon[perm]
     uniq = t.tax_id[np.flatnonzero(np.r_[True, taxon[1:] > np.maximum.accumulate(taxon[:-1])])] if n else t.tax_id
-    data = {"tax_id": _categorical_from_codes(tax, uniq)}
     if t.format == 22:
-        data["tax_name"] = _categorical_from_codes(t.name_code[perm], t.names)
-        data["tax_rank"] = _categorical_from_codes(t.rank_code[perm], t.ranks)
+        cat_id, cat_name, cat_rank, cat_strand = _categoricals(
+            perm, [(taxon, uniq), (t.name_code, t.names), (t.rank_code, t.ranks), (t.strand_code, t.strands)],
+            n_threads)
     else:  # the data/input adapter of counts.read_counts_file: "taxid_<id>", "unknown"
-        data["tax_name"] = _categorical_from_codes(tax, np.array([f"taxid_{v}" for v in uniq], dtype=object))
-        data["tax_rank"] = _const_category("unknown", k)
+        cat_id, cat_name, cat_strand = _categoricals(
+            perm, [(taxon, uniq), (taxon, np.array([f"taxid_{v}" for v in uniq], dtype=object)),
+                   (t.strand_code, t.strands)], n_threads)
+        cat_rank = _const_category("unknown", k)
+    data = {"tax_id": cat_id, "tax_name": cat_name, "tax_rank": cat_rank}
     data["N_alignments"] = nal
-    data["strand"] = _categorical_from_codes(t.strand_code[perm], t.strands)
+    data["strand"] = cat_strand
     data["position"] = pos
     for j, b in enumerate(BASES):
         data[b] = c16[j]
