@@ -58,6 +58,7 @@ struct LocalStrings {
 struct Chunk {
   const char* begin = nullptr;
   const char* end = nullptr;
+  std::string tail;  // the file's last line when it lacks a newline, with one
   int64_t row0 = 0, rows = 0;  // rows: non-blank lines
   LocalStrings str[3];
   int err = 0;
@@ -81,43 +82,44 @@ struct mdi_table {
 
 namespace {
 
-inline bool parse_int(const char*& p, const char* end, int64_t* v) {
+// The scanners below take no end pointer: every line they see ends in '\n'
+// (parse_chunk hands a last line without one over as a copy with it appended),
+// and none of them moves past a '\n', so the newline is the sentinel.
+inline bool parse_int(const char*& p, int64_t* v) {
   bool neg = false;
-  if (p < end && (*p == '-' || *p == '+')) {
+  if (*p == '-' || *p == '+') {
     neg = *p == '-';
     ++p;
   }
   const char* s = p;
   int64_t x = 0;
-  while (p < end && (unsigned)(*p - '0') < 10u) {
+  while ((unsigned)(*p - '0') < 10u) {
     x = x * 10 + (*p - '0');
     ++p;
   }
   if (p == s) return false;
-  if (p < end && *p == '.') {  // tolerate a float rendering of an integer ("12.0")
+  if (*p == '.') {  // tolerate a float rendering of an integer ("12.0")
     ++p;
-    while (p < end && *p == '0') ++p;
-    if (p < end && (unsigned)(*p - '0') < 10u) return false;
+    while (*p == '0') ++p;
+    if ((unsigned)(*p - '0') < 10u) return false;
   }
   *v = neg ? -x : x;
   return true;
 }
 
-inline std::string_view field(const char*& p, const char* end) {
+inline std::string_view field(const char*& p) {
   const char* s = p;
-  while (p < end && *p != '\t' && *p != '\n' && *p != '\r') ++p;
+  while (*p != '\t' && *p != '\n' && *p != '\r') ++p;
   return std::string_view(s, (size_t)(p - s));
 }
 
-inline bool tab(const char*& p, const char* end) {
-  if (p < end && *p == '\t') {
+inline bool tab(const char*& p) {
+  if (*p == '\t') {
     ++p;
     return true;
   }
   return false;
 }
-
-inline bool blank_at(const char* p, const char* end) { return p < end && (*p == '\n' || *p == '\r'); }
 
 int64_t count_rows(const char* p, const char* end) {
   int64_t n = 0;
@@ -136,58 +138,80 @@ struct Out {
   int64_t rows;
 };
 
+// one line [p, its '\n'] into row r; false on a malformed field (col set)
+inline bool parse_line(const char*& p, int format, const Out& o, Chunk* c, int64_t r, int& col) {
+  col = 0;
+  int64_t tid, nal, pos;
+  std::string_view name, rank;
+  if (!parse_int(p, &tid) || !tab(p)) return false;
+  ++col;
+  if (format == 22) {
+    name = field(p);
+    if (!tab(p)) return false;
+    ++col;
+    rank = field(p);
+    if (!tab(p)) return false;
+    ++col;
+  }
+  if (!parse_int(p, &nal) || !tab(p)) return false;
+  ++col;
+  const std::string_view strand = field(p);
+  if (!tab(p)) return false;
+  ++col;
+  if (!parse_int(p, &pos)) return false;
+  ++col;
+  for (int j = 0; j < 16; ++j) {  // column-major: counts[j][rows]
+    int64_t v;
+    if (!tab(p) || !parse_int(p, &v)) return false;
+    o.counts[(int64_t)j * o.rows + r] = v;
+    ++col;
+  }
+  while (*p == '\r') ++p;
+  if (*p != '\n') return false;
+  ++p;
+  o.tax_id[r] = tid;
+  o.nal[r] = nal;
+  o.pos[r] = pos;
+  o.code[MDI_STR_NAME][r] = c->str[MDI_STR_NAME].add(name);
+  o.code[MDI_STR_RANK][r] = c->str[MDI_STR_RANK].add(rank);
+  o.code[MDI_STR_STRAND][r] = c->str[MDI_STR_STRAND].add(strand);
+  return true;
+}
+
 void parse_chunk(Chunk* c, int format, const Out& o) {
   const char* p = c->begin;
   const char* end = c->end;
   int64_t r = c->row0;
   const int64_t rend = c->row0 + c->rows;
-  while (p < end) {
-    if (blank_at(p, end)) {
-      ++p;
-      continue;
+  // a last line without its newline: parsed from a copy that has one (its
+  // string fields then view the copy, which lives as long as the chunk)
+  const char* tail = end;
+  if (end > p && end[-1] != '\n') {
+    const char* q = end;
+    while (q > p && q[-1] != '\n') --q;
+    tail = q;
+    c->tail.assign(q, (size_t)(end - q));
+    c->tail.push_back('\n');
+  }
+  int col = 0;
+  auto bad = [&](int colno) {
+    c->err = MDI_E_PARSE;
+    c->bad_row = r - c->row0;
+    c->bad_col = colno;
+  };
+  for (int part = 0; part < 2; ++part) {
+    const char* q = part == 0 ? p : c->tail.data();
+    const char* qe = part == 0 ? tail : c->tail.data() + c->tail.size();
+    while (q < qe) {
+      if (*q == '\n' || *q == '\r') {  // blank line
+        ++q;
+        continue;
+      }
+      if (r >= rend) return bad(0);  // (rows were counted on the same bytes)
+      if (!parse_line(q, format, o, c, r, col)) return bad(col);
+      ++r;
     }
-    int col = 0;
-    auto bad = [&](int colno) {
-      c->err = MDI_E_PARSE;
-      c->bad_row = r - c->row0;
-      c->bad_col = colno;
-    };
-    if (r >= rend) return bad(0);  // (rows were counted on the same bytes)
-    int64_t tid, nal, pos;
-    std::string_view name, rank;
-    if (!parse_int(p, end, &tid) || !tab(p, end)) return bad(col);
-    ++col;
-    if (format == 22) {
-      name = field(p, end);
-      if (!tab(p, end)) return bad(col);
-      ++col;
-      rank = field(p, end);
-      if (!tab(p, end)) return bad(col);
-      ++col;
-    }
-    if (!parse_int(p, end, &nal) || !tab(p, end)) return bad(col);
-    ++col;
-    const std::string_view strand = field(p, end);
-    if (!tab(p, end)) return bad(col);
-    ++col;
-    if (!parse_int(p, end, &pos)) return bad(col);
-    ++col;
-    for (int j = 0; j < 16; ++j) {  // column-major: counts[j][rows]
-      int64_t v;
-      if (!tab(p, end) || !parse_int(p, end, &v)) return bad(col);
-      o.counts[(int64_t)j * o.rows + r] = v;
-      ++col;
-    }
-    while (p < end && *p == '\r') ++p;
-    if (p < end && *p != '\n') return bad(col);
-    if (p < end) ++p;
-    o.tax_id[r] = tid;
-    o.nal[r] = nal;
-    o.pos[r] = pos;
-    o.code[MDI_STR_NAME][r] = c->str[MDI_STR_NAME].add(name);
-    o.code[MDI_STR_RANK][r] = c->str[MDI_STR_RANK].add(rank);
-    o.code[MDI_STR_STRAND][r] = c->str[MDI_STR_STRAND].add(strand);
-    ++r;
+    if (c->tail.empty()) break;
   }
 }
 
