@@ -6,7 +6,8 @@ call bit for bit:
     fused per-position step of the PPL-1 fit kernel, hpdi_prep_kernel after
     PPL 2);
   * the NULL (legacy default) HIP stream, and a call from another host thread
-    (each thread forks the record assembly onto its own side stream);
+    (the record assembly forks onto the device's one side stream, the fork
+    serialised by a mutex);
   * the call captured into a HIP graph and replayed;
   * garbage-filled workspace and outputs (MAP in both layouts, NUTS): every
     record column equal to a call on zeroed buffers.

@@ -82,6 +82,46 @@ def stages(files, out_dir, inference):
         print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in t.items()}), flush=True)
 
 
+def _trace_wrappers():
+    """Wrap the pipeline's stage functions to record (thread, stage, t0, t1):
+    the per-thread busy time and the critical path of main.main()."""
+    import threading
+
+    from metadamage_amd import counts, fits, io
+
+    events = []
+
+    def wrap(mod, name, label):
+        f = getattr(mod, name)
+
+        def g(*a, **k):
+            t0 = time.perf_counter()
+            try:
+                return f(*a, **k)
+            finally:
+                events.append((threading.current_thread().name, label, t0, time.perf_counter()))
+
+        setattr(mod, name, g)
+
+    wrap(counts, "compute_counts", "ingest")
+    wrap(fits, "pack_counts", "pack")
+    wrap(fits, "fit_packed", "fit")
+    wrap(fits, "make_df_fit_results", "frame_results")
+    wrap(fits, "make_df_fit_predictions", "frame_predictions")
+    wrap(io.Parquet, "save", "parquet")
+    return events
+
+
+def _trace_summary(events, t_start, wall):
+    by = {}
+    for th, label, t0, t1 in events:
+        d = by.setdefault(th, {})
+        d[label] = d.get(label, 0.0) + (t1 - t0)
+    return {"wall_s": round(wall, 3), "threads": {th: {k: round(v, 3) for k, v in d.items()} for th, d in by.items()},
+            "timeline": [[th, label, round(t0 - t_start, 3), round(t1 - t_start, 3)] for th, label, t0, t1 in
+                         sorted(events, key=lambda e: e[2])]}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--files", type=int, default=10)
@@ -90,6 +130,7 @@ def main() -> None:
     ap.add_argument("--dir", default="/tmp/mdfit_c5")
     ap.add_argument("--stages", type=int, default=2, help="files to time stage by stage first (0: none)")
     ap.add_argument("--gen-procs", type=int, default=8)
+    ap.add_argument("--trace", action="store_true", help="print the per-thread stage timeline of the driver run")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -124,11 +165,14 @@ def main() -> None:
     cfg.add_filenames(files)
     if world > 1:
         dist.barrier()
+    events = _trace_wrappers() if a.trace else None
     torch.cuda.synchronize()
     s = time.perf_counter()
     res = driver.main(files, cfg)
     torch.cuda.synchronize()
     wall = time.perf_counter() - s
+    if events is not None and rank == 0:
+        print(json.dumps({"trace": _trace_summary(events, s, wall)}), flush=True)
     taxa = sum(len(r[0]) for r in res.values() if r[0] is not None)
     if world > 1:
         t = torch.tensor([wall, float(taxa)], dtype=torch.float64, device="cuda")
