@@ -70,7 +70,17 @@ __device__ __forceinline__ unsigned long long stamp() {
 }
 #endif
 
-constexpr int kHpdiCtr = 16;  // workspace ints: [16] front-list count, [17] claim counter, [18] back-list count (zeroed by K0)
+// MAP workspace, int32 words of the 256-byte header (zeroed by K0 but the epoch):
+//   [0, 8) the per-XCD all-position task counters (fit_kernel)
+//   [8]    ready-list length (fit_kernel appends a PMD-all mode per taxon)
+//   [9]    hpdi_stream_kernel's item claim counter
+//   [10]   "fit_kernel has started" (hpdi_stream_kernel waits on the list only then)
+//   [16, 19) the wide-window list counters of K4a/K4b (the array entry point)
+//   [60, 62) the call's epoch (uint64), +1 per call: the ready entries' tag
+// then the ready list: double[T][kReadyStride] = (q, A, c, phi, taxon, epoch)
+constexpr int kWsReady = 8, kWsClaim = 9, kWsStarted = 10, kWsEpoch = 60;
+constexpr int kReadyStride = 6;
+constexpr int kHpdiCtr = 16;  // workspace ints: [16] front-list count, [17] claim counter, [18] back-list count
 
 // ---------------------------------------------------------------------------
 // K0: initial points (oracle: init_u)
@@ -83,12 +93,14 @@ __device__ __forceinline__ int kpos(int i) { return i < kNHalf ? i : i - kNHalf;
 // by its own mode when it converged -- the warm start).
 __global__ __launch_bounds__(256) void init_kernel(const uint32_t* __restrict__ gy,
                                                    const uint32_t* __restrict__ gN, int64_t T,
-                                                   double* __restrict__ out, int* __restrict__ ws, int keep_hpdi) {
+                                                   double* __restrict__ out, int* __restrict__ ws) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   // the fit kernel's queue counters (workspace, 256 B): zeroed here instead of
   // by a separate memset launch (stream order puts this before the fit kernel)
-  // (keep_hpdi: the MDFIT_EXP_OVERLAP timing experiment keeps the HPDI list)
-  if (i < 64 && !(keep_hpdi && i >= kHpdiCtr && i < kHpdiCtr + 3)) ws[i] = 0;
+  // -- all but the epoch, which advances by one per call (graph replays
+  // included: this kernel is the call's first node)
+  if (i < 64 && i != kWsEpoch && i != kWsEpoch + 1) ws[i] = 0;
+  if (i == 0) ++*reinterpret_cast<uint64_t*>(ws + kWsEpoch);
   if (i >= MDFIT_NSUBFIT * T) return;
   const int64_t taxon = i / MDFIT_NSUBFIT;
   const int sub = (int)(i % MDFIT_NSUBFIT);  // 0 PMD-all 1 null-all 2 PMD-f 3 PMD-r 4 null-f 5 null-r
@@ -248,8 +260,8 @@ __device__ __forceinline__ void hpdi_position(const HpdiIO& io, int64_t item, bo
 template <int PPL>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_FIT_WAVES_PER_EU)))
 void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN, int64_t T,
-                int max_iter, double tol, double* __restrict__ out, int* __restrict__ ws, float* __restrict__ pred,
-                int per, int* __restrict__ hctr, hpdi::WideRec* __restrict__ hrecs) {
+                int max_iter, double tol, double* __restrict__ out, int* __restrict__ ws,
+                double* __restrict__ ready) {
   static_assert(PPL == 1 || PPL == 2, "points per lane");
   constexpr int kSlot = PPL == 1 ? 32 : 16;  // lanes per slot (one all-position fit or one pair)
   constexpr int kHalf = kSlot / 2;           // lanes per fwd/rev sub-fit of a pair
@@ -299,6 +311,11 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
   pb.k = kB_all;
   pa.pmd = pb.pmd = true;
 
+  // the HPDI stream kernel running beside this one waits only once it has
+  // seen this flag (no wait on a kernel that may not be running)
+  if (blockIdx.x == 0 && lane == 0)
+    __hip_atomic_store(ws + kWsStarted, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t epoch = *reinterpret_cast<const uint64_t*>(ws + kWsEpoch);
   int mode = kIdle;
   int drained = 0, allok = 0;
   // the sub-fit of this lane's half (replicated on its lanes; for an
@@ -594,34 +611,33 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
     const unsigned long long busy = __ballot(running);
     if ((busy & slot_mask) == 0ull) {
       if (mode == kAllFit) {
-        if (PPL == 1 && sub == 0 && hrecs != nullptr) {
-          // the PMD-all fit just ended: the predictive HPDI's per-position step
-          // here (K4a's work, lane = position; the same arithmetic as
-          // theta_kernel + hpdi_prep_kernel), its wide windows to K4b's list
-          HpdiIO io{};
-          io.gN = gN;
-          io.out = out;
-          io.pred = pred;
-          io.per = per;
+        if (sub == 0) {
+          // the PMD-all fit just ended: publish its (q, A, c, phi) -- make_theta's
+          // arithmetic, NaN for invalid input -- as the next entry of the ready
+          // list that hpdi_stream_kernel consumes beside this kernel (the
+          // predictive HPDI, MDFIT-HPDI v1).  Six 8-byte agent-scope (sc1)
+          // stores by lanes 0..5 of the slot, the epoch tag last, behind the
+          // wave's store wait: a reader that sees the tag sees the entry.
           auto sig = [](double v) {
             const double e = exp(-fabs(v));
             const double rr = rcp(1.0 + e);
             return v >= 0.0 ? rr : e * rr;
           };
-          const double q = sig(u[0]), A = sig(u[1]), c = u[2], phi = exp(u[3]) + 2.0;
-          const bool bad = (__ballot(vA_all && pa.y > pa.N) & slot_mask) != 0ull;  // invalid input: NaN windows
-          const bool valid = vA_all && (per == kNPos || colA_all == 0);
-          const int64_t item = per == kNPos ? taxon * kNPos + colA_all : taxon;
-          const double N = pa.N;
-          double a = 0.0, b = 0.0;
-          bool skip = true;
-          if (valid && N > 0.0 && !bad && !isnan(q)) {
-            const double D = fmin(fma(A, powk(1.0 - q, kA_all), c), 1.0);
-            a = D * phi;
-            b = (1.0 - D) * phi;
-            skip = false;
-          }
-          hpdi_position<true>(io, item, valid, skip, N, a, b, T * per, hctr, hrecs);
+          const bool badA = vA_all && pa.y > pa.N;
+          const bool badB = PPL == 2 && vB_all && pb.y > pb.N;
+          const bool bad = (__ballot(badA || badB) & slot_mask) != 0ull;
+          int idx = 0;
+          if (r == 0) idx = atomicAdd(ws + kWsReady, 1);
+          idx = __shfl(idx, leader);
+          double* e = ready + (int64_t)idx * kReadyStride;
+          const double v = r == 0 ? sig(u[0]) : (r == 1 ? sig(u[1]) : (r == 2 ? u[2] : exp(u[3]) + 2.0));
+          if (r < 4) __hip_atomic_store(e + r, bad ? NAN : v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (r == 4)
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(e + 4), (uint64_t)taxon, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (r == 5)
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(e + 5), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         mode = kNextPair;
       } else if (mode == kPairFit) {
@@ -826,30 +842,6 @@ __global__ __launch_bounds__(kWave) void assemble_kernel(
   if (lane == 0) status[t] = st;
 }
 
-// K3a: the PMD-all mode u* -> (q, A, c, phi) into the workspace for K4 (the
-// same arithmetic as make_theta, so K4 sees the values K3 writes to the
-// record); NaN for a taxon with invalid input (y > N somewhere: K3 writes a NaN
-// record for it, K4 then NaN windows).  One thread per taxon.
-__global__ __launch_bounds__(256) void theta_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN,
-                                                    int64_t n_taxa, const double* __restrict__ out,
-                                                    double* __restrict__ theta) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_taxa) return;
-  bool bad = false;
-  for (int i = 0; i < kNPos; ++i) bad = bad || gy[t * kLD + i] > gN[t * kLD + i];
-  const double* dg = out + t * MDFIT_NOUT + MDFIT_F_DIAG;  // sub-fit 0: u*
-  auto sig = [](double v) {
-    const double e = exp(-fabs(v));
-    const double rr = rcp(1.0 + e);
-    return v >= 0.0 ? rr : e * rr;
-  };
-  const double q = sig(dg[0]), A = sig(dg[1]), c = dg[2], phi = exp(dg[3]) + 2.0;
-  theta[t * 4 + 0] = bad ? NAN : q;
-  theta[t * 4 + 1] = bad ? NAN : A;
-  theta[t * 4 + 2] = bad ? NAN : c;
-  theta[t * 4 + 3] = bad ? NAN : phi;
-}
-
 // ---------------------------------------------------------------------------
 // K4: 68 % predictive HPDI (MDFIT-HPDI v1, mdfit_hpdi.h) of the PMD-all mode at
 // every position (fits.py:112-120, 260-261).  K4a: one lane per (taxon,
@@ -934,6 +926,112 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
       hpdi_write<kFit>(io, item, W.P.N, lo, hi);
       busy = false;
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K4 of mdfit_fit_batch: the predictive HPDI streamed beside the fit
+// ---------------------------------------------------------------------------
+// One lane per (taxon, position) item at a time, items enumerated in ready-list
+// order (entry = a PMD-all mode published by fit_kernel as that fit ends, see
+// fit_kernel): a lane claims an item (one atomic per wave-trip), waits for its
+// entry's tag, then runs the position's window -- the greedy when narrow
+// (prep_position), else the wide window's level iterations, one per trip, with
+// the lane refilling when it settles (the K4a / K4b arithmetic: the same
+// windows bit for bit).  Two launches share the claim counter: kEarly on a side
+// stream beside fit_kernel with a small grid (MDFIT_STREAM_WAVES_PER_CU waves
+// per CU; the fit kernel's grid leaves them room), so the HPDI work fills the
+// fit kernel's idle issue slots and its tail; and one after fit_kernel on the
+// caller's stream, full occupancy, for what is left.
+// Waiting: a kEarly wave waits on entries only after it has seen fit_kernel's
+// started flag -- a started fit kernel completes whatever this kernel does,
+// and publishes all T entries -- and exits when the flag has not appeared
+// within ~50 us (its launch may have been queued behind this one: the two
+// streams can share a hardware queue); the late launch never waits.  Every
+// wave exits once the claim counter passes T * per.
+#ifndef MDFIT_STREAM_WAVES_PER_CU
+#define MDFIT_STREAM_WAVES_PER_CU 2
+#endif
+template <bool kEarly>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPDI_WAVES_PER_EU))) void hpdi_stream_kernel(
+    const uint32_t* __restrict__ gN, int64_t T, int per, double* __restrict__ out, float* __restrict__ pred,
+    int* __restrict__ ws, const double* __restrict__ ready) {
+  const int lane = threadIdx.x;
+  if (kEarly) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+    while (__hip_atomic_load(ws + kWsStarted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 5000u) return;  // 50 us: the fit kernel is not running
+      __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  const uint64_t epoch =
+      __hip_atomic_load(reinterpret_cast<const uint64_t*>(ws + kWsEpoch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  HpdiIO io{};
+  io.out = out;
+  io.pred = pred;
+  io.per = per;
+  const int64_t n_items = T * per;
+  hpdi::Wide W;
+  int64_t item = 0, oitem = 0;  // the claimed item; its output index taxon * per + position
+  bool busy = false, pending = false, drained = false;
+  while (true) {
+    const bool need = !busy && !pending && !drained;
+    const unsigned long long m = __ballot(need);
+    if (m != 0ull) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(ws + kWsClaim, __popcll(m));
+      base = __shfl(base, 0);
+      if (need) {
+        const int64_t it = (int64_t)base + __popcll(m & ((1ull << lane) - 1ull));
+        if (it >= n_items) drained = true;
+        else {
+          item = it;
+          pending = true;
+        }
+      }
+    }
+    bool prog = false;
+    if (pending) {
+      const int64_t ei = item / per;
+      const double* e = ready + ei * kReadyStride;
+      const uint64_t tag = __hip_atomic_load(reinterpret_cast<const uint64_t*>(e + 5), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      if (tag == epoch) {
+        const double q = __hip_atomic_load(e + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double A = __hip_atomic_load(e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double c = __hip_atomic_load(e + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double phi = __hip_atomic_load(e + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int64_t taxon = (int64_t)__hip_atomic_load(reinterpret_cast<const uint64_t*>(e + 4), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+        const int i = (int)(item - ei * per);
+        oitem = taxon * per + i;
+        const double N = (double)gN[taxon * kLD + i];
+        double lo = NAN, hi = NAN;
+        bool wide = false;
+        if (N > 0.0 && !isnan(q)) {  // (the arithmetic of hpdi_prep_kernel)
+          const int k = i < kNHalf ? i : i - kNHalf;
+          const double D = fmin(fma(A, powk(1.0 - q, k), c), 1.0);
+          hpdi::WideRec rec;
+          wide = !hpdi::prep_position(N, D * phi, (1.0 - D) * phi, lo, hi, rec);
+          if (wide) hpdi::wide_start(W, rec);
+        }
+        if (wide) busy = true;
+        else hpdi_write<true>(io, oitem, N, lo, hi);
+        pending = false;
+        prog = true;
+      }
+    }
+    if (!__any(busy || pending || !drained)) break;
+    if (busy) {
+      prog = true;
+      if (hpdi::wide_iter(W)) {
+        double lo, hi;
+        hpdi::wide_finish(W, lo, hi);
+        hpdi_write<true>(io, oitem, W.P.N, lo, hi);
+        busy = false;
+      }
+    }
+    if (!__any(prog)) __builtin_amdgcn_s_sleep(8);  // every lane waits on an entry still being fitted
   }
 }
 
@@ -1110,25 +1208,26 @@ int env_int(const char* name, int dflt) {
   return e ? std::atoi(e) : dflt;
 }
 
-// MAP workspace: 256 B of counters, the PMD-all (q, A, c, phi) of every taxon
-// (K3a -> K4; n_theta = n_taxa, 0 for the array entry point), then the HPDI
-// wide-window records
-double* theta_buf(void* ws) { return reinterpret_cast<double*>(static_cast<char*>(ws) + 256); }
-mdfit::hpdi::WideRec* hpdi_recs(void* ws, int64_t n_theta) {
-  return reinterpret_cast<mdfit::hpdi::WideRec*>(static_cast<char*>(ws) + 256 + n_theta * 4 * (int64_t)sizeof(double));
+// MAP workspace: the 256-byte header (mdfit::kWs*), then the ready list
+// (kReadyStride doubles per taxon); the array entry point (mdfit_hpdi68) puts
+// its K4a / K4b wide-window records right after the header
+double* ready_buf(void* ws) { return reinterpret_cast<double*>(static_cast<char*>(ws) + 256); }
+mdfit::hpdi::WideRec* hpdi_recs(void* ws) {
+  return reinterpret_cast<mdfit::hpdi::WideRec*>(static_cast<char*>(ws) + 256);
 }
 
-// The side stream of mdfit_fit_batch's fork (the record assembly runs there
-// beside the HPDI kernels) and its fork / join events: one set per device,
-// created on first use and kept for the process (a bounded 1 stream per
-// device, not one per calling host thread); the stream non-blocking (ordered
-// against the caller's stream by the events only).  The events are shared, so
-// a call holds the device's mutex from the fork record to the join wait: a
-// wait binds to the record enqueued before it, and another thread's record in
-// between would rebind it.
+// The side streams of mdfit_fit_batch's forks -- [0] the HPDI stream kernel
+// beside the fit kernel, [1] the record assembly beside the late HPDI launch --
+// and their fork / join events: one set per device, created on first use and
+// kept for the process (bounded: 2 streams per device, not per calling host
+// thread); the streams non-blocking (ordered against the caller's stream by the
+// events only).  The events are shared, so a call holds the device's mutex from
+// its first fork record to its last join wait: a wait binds to the record
+// enqueued before it, and another thread's record in between would rebind it.
 struct Fork {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
+  hipStream_t s[2] = {nullptr, nullptr};
+  hipEvent_t fork[2] = {nullptr, nullptr}, join[2] = {nullptr, nullptr};
+  bool ok = false;
   std::mutex mu;
 };
 Fork* side_fork() {
@@ -1139,41 +1238,38 @@ Fork* side_fork() {
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
   Fork& x = f[dev];
   std::lock_guard<std::mutex> g(make_mu);
-  if (x.s == nullptr) {
-    if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess) {
-      (void)hipStreamDestroy(x.s);
-      if (x.fork) (void)hipEventDestroy(x.fork);
-      x.s = nullptr;
-      x.fork = x.join = nullptr;
-      return nullptr;
-    }
+  if (!x.ok) {
+    bool ok = true;
+    for (int k = 0; k < 2 && ok; ++k)
+      ok = (x.s[k] != nullptr || hipStreamCreateWithFlags(&x.s[k], hipStreamNonBlocking) == hipSuccess) &&
+           (x.fork[k] != nullptr || hipEventCreateWithFlags(&x.fork[k], hipEventDisableTiming) == hipSuccess) &&
+           (x.join[k] != nullptr || hipEventCreateWithFlags(&x.join[k], hipEventDisableTiming) == hipSuccess);
+    if (!ok) return nullptr;  // (what was created is kept for the next try)
+    x.ok = true;
   }
   return &x;
 }
 
-// The fork's scope: holds the device's fork mutex and, when the fork was
-// opened, joins the side stream back into the caller's stream on EVERY exit
-// of mdfit_fit_batch -- error returns included -- so no kernel of the call is
-// still running on the side stream when the caller (whose allocator orders
-// frees against its own stream only) gets control back, and a graph capture
-// never ends with an open fork.
+// One fork's scope: when opened, joins side stream k back into the caller's
+// stream on EVERY exit of mdfit_fit_batch -- error returns included -- so no
+// kernel of the call is still running on a side stream when the caller (whose
+// allocator orders frees against its own stream only) gets control back, and a
+// graph capture never ends with an open fork.  (The device's mutex is held by
+// the call around all its forks.)
 struct ForkScope {
   Fork* fk;
   hipStream_t s;
+  int k;
   bool open = false;
-  std::unique_lock<std::mutex> lk;
-  ForkScope(Fork* f, hipStream_t st) : fk(f), s(st) {
+  ForkScope(Fork* f, hipStream_t st, int which) : fk(f), s(st), k(which) {
     if (fk == nullptr) return;
-    lk = std::unique_lock<std::mutex>(fk->mu);
-    open = hipEventRecord(fk->fork, s) == hipSuccess && hipStreamWaitEvent(fk->s, fk->fork, 0) == hipSuccess;
+    open = hipEventRecord(fk->fork[k], s) == hipSuccess && hipStreamWaitEvent(fk->s[k], fk->fork[k], 0) == hipSuccess;
   }
-  hipStream_t side() const { return open ? fk->s : s; }  // no side stream: everything in order on s
+  hipStream_t side() const { return open ? fk->s[k] : s; }  // no side stream: everything in order on s
   int join() {
     if (!open) return 0;
     open = false;
-    if (hipEventRecord(fk->join, fk->s) != hipSuccess || hipStreamWaitEvent(s, fk->join, 0) != hipSuccess)
+    if (hipEventRecord(fk->join[k], fk->s[k]) != hipSuccess || hipStreamWaitEvent(s, fk->join[k], 0) != hipSuccess)
       return set_err(MDFIT_E_HIP, "stream join");
     return 0;
   }
@@ -1254,9 +1350,9 @@ int64_t mdfit_workspace_bytes(int64_t n_taxa, const mdfit_opts* opts) {
   mdfit_default_opts(&o);
   if (opts) o = *opts;
   if (o.mode == MDFIT_MODE_NUTS) return mdfit::nuts::workspace_bytes(n_taxa, o.num_samples);
-  // the 8 per-XCD queue counters + the HPDI list counters (int32, 256 B), then
-  // room for every position's wide-window record (MDFIT-HPDI v1)
-  return 256 + n_taxa * 4 * (int64_t)sizeof(double) + n_taxa * mdfit::kNPos * (int64_t)sizeof(mdfit::hpdi::WideRec);
+  // the 256-byte header (counters, flags, the epoch), then the ready list of
+  // PMD-all modes the HPDI stream kernel consumes: 48 B per taxon
+  return 256 + n_taxa * mdfit::kReadyStride * (int64_t)sizeof(double);
 }
 
 int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t n_taxa,
@@ -1271,9 +1367,8 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   if (opts) o = *opts;
   if (o.mode != MDFIT_MODE_MAP && o.mode != MDFIT_MODE_NUTS) return set_err(MDFIT_E_ARG, "unsupported mode");
   if (o.max_iter < 1) return set_err(MDFIT_E_ARG, "max_iter < 1");
-  // the HPDI list counters and indices are int32 over T * 30 positions, and the
-  // MAP workspace holds ~4.8 KB per taxon (mdfit_workspace_bytes): 2^25 taxa
-  // (1e9 positions, ~162 GB of workspace) per call at most
+  // the HPDI item counters are int32 over T * 30 positions: 2^25 taxa (1e9
+  // positions) per call at most
   if (n_taxa > ((int64_t)1 << 25)) return set_err(MDFIT_E_ARG, "n_taxa exceeds 2^25 per call");
   hipStream_t s = (hipStream_t)hip_stream;
   int* ws = (int*)workspace;
@@ -1286,74 +1381,70 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
     return 0;
   }
   const int64_t n_init = MDFIT_NSUBFIT * n_taxa;
-  // MDFIT_EXP_OVERLAP=1 (timing experiment only, results of the HPDI columns
-  // meaningless): K4b runs on the side stream beside the fit kernel, draining
-  // the wide-window list the PREVIOUS call of the same batch left in the
-  // workspace, while the fit kernel skips its fused HPDI step -- the call time
-  // a fit/HPDI overlap could reach at PPL 1
-  const bool exp_overlap = env_int("MDFIT_EXP_OVERLAP", 0) == 1 && n_taxa < kPpl2MinTaxa;
-  mdfit::hpdi::WideRec* recs0 = hpdi_recs(workspace, n_taxa);
-  if (exp_overlap && hipMemsetAsync(ws + mdfit::kHpdiCtr + 1, 0, 4, s) != hipSuccess)
-    return set_err(MDFIT_E_HIP, "memset");
-  ForkScope fork0(exp_overlap ? side_fork() : nullptr, s);
-  if (exp_overlap) {
-    mdfit::HpdiIO io{};
-    io.gN = N;
-    io.out = out;
-    io.pred = pred;
-    io.per = pred != nullptr ? mdfit::kNPos : 1;
-    if (int rc = launch_hpdi<true>(io, n_taxa * io.per, ws + mdfit::kHpdiCtr, recs0, fork0.side(), false)) return rc;
-  }
   hipLaunchKernelGGL(mdfit::init_kernel, dim3((unsigned)((n_init + 255) / 256)), dim3(256), 0, s, y, N,
-                     n_taxa, out, ws, exp_overlap ? 1 : 0);
+                     n_taxa, out, ws);
   if (int rc = check_launch("init_kernel")) return rc;
   // lane layout of the fit kernel (bitwise-identical results): 2 points per
   // lane for batches that fill the chip several times over, 1 below (lower
   // latency per evaluation).  MDFIT_FIT_PPL=1|2 overrides (development A/B).
   int ppl = n_taxa >= kPpl2MinTaxa ? 2 : 1;
   if (const char* e = std::getenv("MDFIT_FIT_PPL")) ppl = std::atoi(e) == 2 ? 2 : 1;
-  prof_record(1, s);
   const int per = pred != nullptr ? mdfit::kNPos : 1;
-  mdfit::hpdi::WideRec* recs = hpdi_recs(workspace, n_taxa);
-  int* hctr = ws + mdfit::kHpdiCtr;
-  if (ppl == 2) {
-    const int64_t g = fit_grid(mdfit::fit_kernel<2>, 2 * n_taxa, 4, env_int("MDFIT_FIT_WAVES_PER_CU", 0));
-    hipLaunchKernelGGL(mdfit::fit_kernel<2>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, y, N, n_taxa,
-                       o.max_iter, o.tol_step, out, ws, pred, per, hctr, (mdfit::hpdi::WideRec*)nullptr);
-  } else {
-    // PPL 1 also runs the HPDI's per-position step (K4a) as each PMD-all fit ends
-    const int64_t g = fit_grid(mdfit::fit_kernel<1>, 2 * n_taxa, 2, env_int("MDFIT_FIT_WAVES_PER_CU", 0));
-    hipLaunchKernelGGL(mdfit::fit_kernel<1>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, y, N, n_taxa,
-                       o.max_iter, o.tol_step, out, ws, pred, per, hctr, exp_overlap ? nullptr : recs);
+  const int64_t n_items = n_taxa * per;
+  double* ready = ready_buf(workspace);
+  // the call's forks share the device's events: hold its mutex throughout
+  // (declared before the scopes, so it is released after their joins)
+  Fork* fk = side_fork();
+  std::unique_lock<std::mutex> fork_lock;
+  if (fk != nullptr) fork_lock = std::unique_lock<std::mutex>(fk->mu);
+  // K4 (early): the predictive HPDI streamed beside the fit kernel, on side
+  // stream 0 from after K0; its grid -- MDFIT_STREAM_WAVES_PER_CU waves per CU
+  // -- is the room the fit kernel's grid leaves
+  const int early_per_cu = fk != nullptr ? env_int("MDFIT_STREAM_WAVES_PER_CU", MDFIT_STREAM_WAVES_PER_CU) : 0;
+  ForkScope fork_hp(early_per_cu > 0 ? fk : nullptr, s, 0);
+  if (early_per_cu > 0) {
+    const int64_t g = fit_grid(mdfit::hpdi_stream_kernel<true>, n_items, mdfit::kWave, early_per_cu);
+    hipLaunchKernelGGL(mdfit::hpdi_stream_kernel<true>, dim3((unsigned)g), dim3(mdfit::kWave), 0, fork_hp.side(), N,
+                       n_taxa, per, out, pred, ws, (const double*)ready);
+    if (int rc = check_launch("hpdi_stream_kernel")) return rc;
+  }
+  prof_record(1, s);
+  {
+    int occ = 8;  // waves per CU the fit kernel may take: its occupancy, less the HPDI stream's
+    const int cap_env = env_int("MDFIT_FIT_WAVES_PER_CU", 0);
+    if (ppl == 2) {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, mdfit::fit_kernel<2>, mdfit::kWave, 0) != hipSuccess) occ = 8;
+      const int cap = cap_env > 0 ? cap_env : std::max(1, occ - early_per_cu);
+      const int64_t g = fit_grid(mdfit::fit_kernel<2>, 2 * n_taxa, 4, cap);
+      hipLaunchKernelGGL(mdfit::fit_kernel<2>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, y, N, n_taxa,
+                         o.max_iter, o.tol_step, out, ws, ready);
+    } else {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, mdfit::fit_kernel<1>, mdfit::kWave, 0) != hipSuccess) occ = 8;
+      const int cap = cap_env > 0 ? cap_env : std::max(1, occ - early_per_cu);
+      const int64_t g = fit_grid(mdfit::fit_kernel<1>, 2 * n_taxa, 2, cap);
+      hipLaunchKernelGGL(mdfit::fit_kernel<1>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, y, N, n_taxa,
+                         o.max_iter, o.tol_step, out, ws, ready);
+    }
   }
   if (int rc = check_launch("fit_kernel")) return rc;
   prof_record(2, s);
-  // (PPL 2: K3a, the PMD-all mode for K4a), then a fork: the record assembly
-  // (K3) on the side stream, the predictive HPDI (K4a, K4b) on the caller's;
-  // they write disjoint fields of the record and join before the call returns
-  double* theta = theta_buf(workspace);
-  if (ppl == 2) {
-    hipLaunchKernelGGL(mdfit::theta_kernel, dim3((unsigned)((n_taxa + 255) / 256)), dim3(256), 0, s, y, N, n_taxa,
-                       out, theta);
-    if (int rc = check_launch("theta_kernel")) return rc;
-  }
-  ForkScope fork(exp_overlap ? nullptr : side_fork(), s);
-  hipStream_t sa = fork.side();
-  hipLaunchKernelGGL(mdfit::assemble_kernel, dim3((unsigned)n_taxa), dim3(mdfit::kWave), 0, sa, y, N,
+  // then a fork: the record assembly (K3) on side stream 1, the HPDI's late
+  // launch on the caller's stream (full occupancy, draining what the early
+  // one left); they write disjoint fields of the record and join before the
+  // call returns
+  ForkScope fork_as(fk, s, 1);
+  hipLaunchKernelGGL(mdfit::assemble_kernel, dim3((unsigned)n_taxa), dim3(mdfit::kWave), 0, fork_as.side(), y, N,
                      mm, n_taxa, out, pred, status);
   if (int rc = check_launch("assemble_kernel")) return rc;
   {
-    mdfit::HpdiIO io{};
-    io.gN = N;
-    io.theta = theta;
-    io.out = out;
-    io.pred = pred;
-    io.per = per;
-    if (!exp_overlap)
-      if (int rc = launch_hpdi<true>(io, n_taxa * io.per, hctr, recs, s, ppl == 2)) return rc;
+    const int64_t g = fit_grid(mdfit::hpdi_stream_kernel<false>, n_items, mdfit::kWave,
+                               env_int("MDFIT_HPDI_WAVES_PER_CU", 0));
+    hipLaunchKernelGGL(mdfit::hpdi_stream_kernel<false>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, N, n_taxa, per,
+                       out, pred, ws, (const double*)ready);
+    if (int rc = check_launch("hpdi_stream_kernel")) return rc;
   }
-  if (int rc = fork.join()) return rc;
-  if (int rc = fork0.join()) return rc;
+  if (int rc = fork_as.join()) return rc;
+  if (int rc = fork_hp.join()) return rc;
   prof_record(3, s);
   if (g_prof.on && g_prof.n < kProfMax) ++g_prof.n;
   return 0;
@@ -1395,7 +1486,7 @@ int mdfit_hpdi68(const double* N, const double* alpha, const double* beta, int64
   io.b = beta;
   io.lo = lo;
   io.hi = hi;
-  int rc = launch_hpdi<false>(io, n, static_cast<int*>(ws) + mdfit::kHpdiCtr, hpdi_recs(ws, 0), s);
+  int rc = launch_hpdi<false>(io, n, static_cast<int*>(ws) + mdfit::kHpdiCtr, hpdi_recs(ws), s);
   (void)hipFreeAsync(ws, s);
   return rc;
 }

@@ -172,3 +172,35 @@ def test_dirty_workspace_and_outputs(torch_dev, monkeypatch, mode, ppl):
         assert np.array_equal(dirty.out.cpu().numpy(), clean.out.cpu().numpy(), equal_nan=True)
         assert np.array_equal(dirty.pred.cpu().numpy(), clean.pred.cpu().numpy(), equal_nan=True)
         assert np.array_equal(dirty.status.cpu().numpy(), clean.status.cpu().numpy())
+
+
+@pytest.mark.parametrize("ppl", ["1", "2"])
+def test_hpdi_stream_beside_the_fit_same_record(torch_dev, monkeypatch, ppl):
+    """The predictive HPDI streamed beside the fit kernel (early launch on a
+    side stream, waiting on the ready list) gives the record of the HPDI run
+    after the fit (MDFIT_STREAM_WAVES_PER_CU=0), bit for bit, with and without
+    predictions, and in both lane layouts."""
+    torch = torch_dev
+    from metadamage_amd import _lib, engine
+    from metadamage_amd.synthetic import generate
+
+    monkeypatch.setenv("MDFIT_FIT_PPL", ppl)
+    b = generate(4_000, seed=23)
+    ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm)
+    opts = _lib.default_opts()
+    recs = []
+    for early in ("0", "2", "4"):
+        monkeypatch.setenv("MDFIT_STREAM_WAVES_PER_CU", early)
+        for with_pred in (True, False):
+            r = engine.fit_batch_device(ty, tN, tm, opts, engine.alloc_outputs(4_000, with_pred=with_pred, opts=opts))
+            torch.cuda.synchronize()
+            recs.append((early, with_pred, r.out.cpu().numpy()[:, :32], None if r.pred is None else r.pred.cpu().numpy(),
+                         r.status.cpu().numpy()))
+    base = {wp: rec for e, wp, *rec in recs if e == "0"}
+    for e, wp, out, pred, st in recs:
+        o0, p0, s0 = base[wp]
+        assert np.array_equal(out, o0, equal_nan=True), (e, wp)
+        assert np.array_equal(st, s0), (e, wp)
+        if wp:
+            assert np.array_equal(pred, p0, equal_nan=True), (e, wp)
+    assert np.isfinite(base[True][0][:, 2:4]).mean() > 0.99

@@ -1,8 +1,9 @@
-"""Development timing experiment (DESIGN.md §11 lead "fit / HPDI overlap"):
-the C2 call time with the fit kernel's grid capped per CU, and with K4b run
-beside the fit kernel on the previous call's wide-window list
-(MDFIT_EXP_OVERLAP=1, HPDI columns meaningless there).  Prints one JSON line
-per configuration.
+"""Development timing A/B of the fit / HPDI overlap: the MAP
+call time at a batch size for several grids of the HPDI stream kernel's early
+launch beside the fit kernel (MDFIT_STREAM_WAVES_PER_CU; 0 = none, the HPDI
+then runs after the fit) and of the fit kernel (MDFIT_FIT_WAVES_PER_CU).
+Every configuration must give the same record (checked).  One JSON line per
+configuration.
 
     python tools/overlap_exp.py [--taxa 10000]
 """
@@ -11,6 +12,8 @@ from __future__ import annotations
 
 import argparse
 import json
+
+import numpy as np
 import os
 import sys
 import time
@@ -35,19 +38,16 @@ def main() -> None:
     opts = _lib.default_opts(mode=_lib.MODE_MAP)
     fb = engine.alloc_outputs(a.taxa, opts=opts)
     stream = torch.cuda.current_stream()
-    configs = [("base", {}), ("fit4", {"MDFIT_FIT_WAVES_PER_CU": "4"}),
-               ("exp", {"MDFIT_EXP_OVERLAP": "1"}),
-               ("exp_fit4_hp4", {"MDFIT_EXP_OVERLAP": "1", "MDFIT_FIT_WAVES_PER_CU": "4", "MDFIT_HPDI_WAVES_PER_CU": "4"}),
-               ("exp_fit4", {"MDFIT_EXP_OVERLAP": "1", "MDFIT_FIT_WAVES_PER_CU": "4"}),
-               ("exp_hp4", {"MDFIT_EXP_OVERLAP": "1", "MDFIT_HPDI_WAVES_PER_CU": "4"}),
-               ("exp_fit6_hp2", {"MDFIT_EXP_OVERLAP": "1", "MDFIT_FIT_WAVES_PER_CU": "6", "MDFIT_HPDI_WAVES_PER_CU": "2"}),
-               ("base_again", {})]
+    configs = [("default", {}), ("no_early", {"MDFIT_STREAM_WAVES_PER_CU": "0"}),
+               ("early1", {"MDFIT_STREAM_WAVES_PER_CU": "1"}), ("early3", {"MDFIT_STREAM_WAVES_PER_CU": "3"}),
+               ("early4", {"MDFIT_STREAM_WAVES_PER_CU": "4"}),
+               ("early2_fit8", {"MDFIT_STREAM_WAVES_PER_CU": "2", "MDFIT_FIT_WAVES_PER_CU": "8"}),
+               ("default_again", {})]
     keys = {k for _, e in configs for k in e}
+    ref = None
     for name, env in configs:
         for k in keys:
             os.environ.pop(k, None)
-        # one normal call first: the list the experiment drains
-        engine.fit_batch_device(ty, tN, tm, opts, fb, stream=stream)
         os.environ.update(env)
         for _ in range(3):
             engine.fit_batch_device(ty, tN, tm, opts, fb, stream=stream)
@@ -60,8 +60,13 @@ def main() -> None:
         dt = (time.perf_counter() - t0) / a.steps
         _, fit_ms, n = engine.profile_read()
         engine.profile_enable(False)
-        print(json.dumps({"config": name, "env": env, "call_ms": round(dt * 1e3, 4),
-                          "fit_kernel_ms": round(fit_ms / n, 4), "fits_per_s": round(a.taxa / dt, 1)}), flush=True)
+        rec = (fb.out[:, :25].cpu().numpy(), fb.pred.cpu().numpy(), fb.status.cpu().numpy())
+        if ref is None:
+            ref = rec
+        same = all(np.array_equal(x, y, equal_nan=True) for x, y in zip(rec, ref))
+        print(json.dumps({"config": name, "env": env, "taxa": a.taxa, "call_ms": round(dt * 1e3, 4),
+                          "fit_kernel_ms": round(fit_ms / n, 4), "fits_per_s": round(a.taxa / dt, 1),
+                          "same_record": same}), flush=True)
 
 
 if __name__ == "__main__":
