@@ -60,6 +60,7 @@ NODE_GPUS = 8  # one MI355X node
 #              3x30x4 + status 4 out
 ALG_BYTES_PER_TAXON = 240 + 208
 FIT_BYTES_PER_TAXON = 240 + 192 + 384
+READY_BYTES_PER_TAXON = 48
 CALL_BYTES_PER_TAXON = 240 + 1440 + 200 + 360 + 4
 NPTS = np.array([30, 30, 15, 15, 15, 15])
 NPTS_POS = 30  # predictive windows per taxon
@@ -290,15 +291,10 @@ def main():
         k_avg_s = fit_ms_sum / n_calls / 1e3
         call_avg_s = call_ms_sum / n_calls / 1e3
         achieved = ALG_BYTES_PER_TAXON * T / k_avg_s / 1e9
-        # the fit kernel's hand-off as built: the record, and at PPL 1 (the
-        # library's layout below 35k taxa) the fused HPDI step's wide-window
-        # list (its length from the workspace counters) and greedy bounds
-        wsi = fb.workspace[:256].view(torch.int32).cpu().numpy()
-        n_wide = int(wsi[16]) + int(wsi[18])
-        ppl_env = os.environ.get("MDFIT_FIT_PPL")
-        fused_prep = (int(ppl_env) != 2) if ppl_env else T < 35_000
-        inter_bytes = FIT_BYTES_PER_TAXON * T + ((160 * n_wide + 8 * (NPTS_POS * T - n_wide) + 16 * T)
-                                                 if fused_prep else 0)
+        # the fit kernel's hand-off as built: the record (K0 -> K1 -> K3), and
+        # the ready list the HPDI stream kernel consumes beside it (one 48 B
+        # entry per taxon: the PMD-all mode, the taxon index, the epoch tag)
+        inter_bytes = FIT_BYTES_PER_TAXON * T + READY_BYTES_PER_TAXON * T
         traffic = pmc_traffic("fit_kernel", T)
         # compute roofline: register-only probe of the same point evaluation
         n_waves, iters = 256 * 16, 64
@@ -357,12 +353,9 @@ def main():
                     "bytes_per_taxon": round(inter_bytes / T, 1),
                     "bytes_per_launch": inter_bytes,
                     "achieved": round(inter_bytes / k_avg_s / 1e9, 3),
-                    "wide_windows": n_wide,
                     "note": "what the kernel moves as built: y,N + the 6 initial points in, the 6 sub-fit records "
-                    "out (816 B/taxon: the K0 -> K1 -> K3 hand-off through the record)" + (
-                        "; plus, PPL 1, the fused predictive-HPDI step's output: a 160 B record per wide window "
-                        "(the hand-off to hpdi_wide_kernel), 8 B of bounds per greedy window, the 2 HPDI columns"
-                        if fused_prep else ""),
+                    "out (816 B/taxon: the K0 -> K1 -> K3 hand-off through the record), plus the 48 B ready-list "
+                    "entry per taxon (the PMD-all mode handed to the HPDI stream kernel running beside it)",
                 },
                 "call_ms_avg": round(call_avg_s * 1e3, 4),
                 "call_bytes_per_taxon": CALL_BYTES_PER_TAXON,

@@ -111,6 +111,12 @@ int mdi_codes(int64_t n_keep, const int64_t* perm, int n_cols, const int32_t* co
               int n_threads, int32_t* const* out, uint8_t* const* used);
 int mdi_remap(int64_t n, int n_cols, int32_t* const* codes, const int32_t* const* remap, int n_threads);
 
+/* Worker threads the library uses when a call passes n_threads <= 0: the
+ * process's CPU share -- OMP_NUM_THREADS when set (a GPU box grants 16 cores
+ * per GPU and sets it), else the CPUs of the affinity mask -- never the whole
+ * machine's hardware_concurrency (256 on an 8-GPU node: oversubscription). */
+int mdi_default_threads(void);
+
 /* message of the last failed mdi_select / mdi_gather on this thread */
 const char* mdi_counts_error(void);
 

@@ -167,7 +167,7 @@ int mdi_gather(int64_t rows, const int64_t* perm, int64_t n_keep, const int64_t*
   const Rows R{rows, nullptr, n_alignments, position, counts16, strand_code, code_is_fwd, n_codes};
   const int ref_base[2] = {kf / 4, kr / 4};
   const int sub[2] = {kf, kr};
-  int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+  int nt = n_threads > 0 ? n_threads : mdi_default_threads();
   if (nt < 1) nt = 1;
   if (n_keep < (int64_t)nt * 65536) nt = (int)std::max<int64_t>(1, n_keep / 65536);
   if (nt > 64) nt = 64;
@@ -224,7 +224,7 @@ const char* mdi_counts_error(void) { return g_cerr; }
 
 namespace {
 int pool_size(int n_threads, int64_t n) {
-  int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+  int nt = n_threads > 0 ? n_threads : mdi_default_threads();
   if (nt < 1) nt = 1;
   if (n < (int64_t)nt * 65536) nt = (int)std::max<int64_t>(1, n / 65536);
   return nt > 64 ? 64 : nt;
@@ -359,7 +359,7 @@ void noise_one(const uint32_t* mm, double* out3) {
 extern "C" int mdi_noise(const uint32_t* mm, int64_t n_taxa, int n_threads, double* out3) {
   if (n_taxa < 0 || (n_taxa > 0 && (!mm || !out3))) return MDI_E_ARG;
   if (n_taxa == 0) return 0;
-  int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+  int nt = n_threads > 0 ? n_threads : mdi_default_threads();
   if (nt < 1) nt = 1;
   if ((int64_t)nt > (n_taxa + 511) / 512) nt = (int)((n_taxa + 511) / 512);
   std::vector<std::thread> pool;

@@ -12,11 +12,13 @@
 #include "../../include/mdingest.h"
 
 #include <fcntl.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <string_view>
@@ -227,6 +229,21 @@ void parallel_chunks(std::vector<Chunk>& chunks, F f) {
 
 extern "C" {
 
+int mdi_default_threads(void) {
+  if (const char* e = std::getenv("OMP_NUM_THREADS")) {
+    const int v = std::atoi(e);
+    if (v > 0) return v;
+  }
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) {
+    const int c = CPU_COUNT(&set);
+    if (c > 0) return c;
+  }
+  const int h = (int)std::thread::hardware_concurrency();
+  return h > 0 ? h : 1;
+}
+
 int mdi_open(const char* path, int n_threads, mdi_table** out) {
   if (!path || !out) return fail(MDI_E_ARG, "null argument");
   *out = nullptr;
@@ -264,7 +281,7 @@ int mdi_open(const char* path, int n_threads, mdi_table** out) {
     }
   }
   t->data = p;
-  int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+  int nt = n_threads > 0 ? n_threads : mdi_default_threads();
   if (nt < 1) nt = 1;
   const size_t span = (size_t)(end - p);
   if (span < ((size_t)1 << 20)) nt = 1;
