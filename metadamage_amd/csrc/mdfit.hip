@@ -261,7 +261,7 @@ template <int PPL>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_FIT_WAVES_PER_EU)))
 void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN, int64_t T,
                 int max_iter, double tol, double* __restrict__ out, int* __restrict__ ws,
-                double* __restrict__ ready) {
+                double* __restrict__ ready, int base_prio) {
   static_assert(PPL == 1 || PPL == 2, "points per lane");
   constexpr int kSlot = PPL == 1 ? 32 : 16;  // lanes per slot (one all-position fit or one pair)
   constexpr int kHalf = kSlot / 2;           // lanes per fwd/rev sub-fit of a pair
@@ -603,8 +603,10 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
     // waves holding a long fit (the critical path of small batches) win issue
     // arbitration: +5 % at C2, no change at 100k taxa (A/B of thresholds
     // 12/15/20/30 and of chain- vs fit-length counting: 15 by fit length best)
+    // (base_prio: every fit wave above the HPDI stream kernel's waves beside it)
     if (__any(running && evals >= 2 * kPrioEvals)) __builtin_amdgcn_s_setprio(3);
     else if (__any(running && evals >= kPrioEvals)) __builtin_amdgcn_s_setprio(2);
+    else if (base_prio) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
     // a slot is free when neither half is running: an all-position fit then
     // continues with its pair, a pair with the next task
@@ -1410,6 +1412,7 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   }
   prof_record(1, s);
   {
+    const int fit_prio = env_int("MDFIT_FIT_BASE_PRIO", 0) != 0 ? 1 : 0;
     int occ = 8;  // waves per CU the fit kernel may take: its occupancy, less the HPDI stream's
     const int cap_env = env_int("MDFIT_FIT_WAVES_PER_CU", 0);
     if (ppl == 2) {
@@ -1417,13 +1420,13 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
       const int cap = cap_env > 0 ? cap_env : std::max(1, occ - early_per_cu);
       const int64_t g = fit_grid(mdfit::fit_kernel<2>, 2 * n_taxa, 4, cap);
       hipLaunchKernelGGL(mdfit::fit_kernel<2>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, y, N, n_taxa,
-                         o.max_iter, o.tol_step, out, ws, ready);
+                         o.max_iter, o.tol_step, out, ws, ready, fit_prio);
     } else {
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, mdfit::fit_kernel<1>, mdfit::kWave, 0) != hipSuccess) occ = 8;
       const int cap = cap_env > 0 ? cap_env : std::max(1, occ - early_per_cu);
       const int64_t g = fit_grid(mdfit::fit_kernel<1>, 2 * n_taxa, 2, cap);
       hipLaunchKernelGGL(mdfit::fit_kernel<1>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, y, N, n_taxa,
-                         o.max_iter, o.tol_step, out, ws, ready);
+                         o.max_iter, o.tol_step, out, ws, ready, fit_prio);
     }
   }
   if (int rc = check_launch("fit_kernel")) return rc;

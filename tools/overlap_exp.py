@@ -42,6 +42,8 @@ def main() -> None:
                ("early1", {"MDFIT_STREAM_WAVES_PER_CU": "1"}), ("early3", {"MDFIT_STREAM_WAVES_PER_CU": "3"}),
                ("early4", {"MDFIT_STREAM_WAVES_PER_CU": "4"}),
                ("early2_fit8", {"MDFIT_STREAM_WAVES_PER_CU": "2", "MDFIT_FIT_WAVES_PER_CU": "8"}),
+               ("prio1", {"MDFIT_FIT_BASE_PRIO": "1"}),
+               ("early4_prio1", {"MDFIT_STREAM_WAVES_PER_CU": "4", "MDFIT_FIT_BASE_PRIO": "1"}),
                ("default_again", {})]
     keys = {k for _, e in configs for k in e}
     ref = None
