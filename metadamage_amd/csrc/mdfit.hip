@@ -70,16 +70,21 @@ __device__ __forceinline__ unsigned long long stamp() {
 }
 #endif
 
-// MAP workspace, int32 words of the 256-byte header (zeroed by K0 but the epoch):
+// MAP workspace, int32 words of the 256-byte header (zeroed by K0):
 //   [0, 8) the per-XCD all-position task counters (fit_kernel)
 //   [8]    ready-list length (fit_kernel appends a PMD-all mode per taxon)
 //   [9]    hpdi_stream_kernel's item claim counter
 //   [10]   "fit_kernel has started" (hpdi_stream_kernel waits on the list only then)
 //   [16, 19) the wide-window list counters of K4a/K4b (the array entry point)
-//   [60, 62) the call's epoch (uint64), +1 per call: the ready entries' tag
-// then the ready list: double[T][kReadyStride] = (q, A, c, phi, taxon, epoch)
-constexpr int kWsReady = 8, kWsClaim = 9, kWsStarted = 10, kWsEpoch = 60;
+// then the ready list: double[T][kReadyStride] = (q, A, c, phi, taxon, tag),
+// zeroed by K0 every call (so no entry of an earlier call or of whatever the
+// buffer held before can pass for a published one: a tag is only ever
+// kReadyTag once this call's fit kernel has written that entry)
+//   [11]   corrupt ready entries met by hpdi_stream_kernel (0; a diagnostic)
+constexpr int kWsReady = 8, kWsClaim = 9, kWsStarted = 10, kWsBad = 11;
 constexpr int kReadyStride = 6;
+static_assert(kReadyStride == MDFIT_NSUBFIT, "K0 zeroes the ready list with one thread per (taxon, sub-fit)");
+constexpr uint64_t kReadyTag = 0x4D44464954524459ull;  // "MDFITRDY"
 constexpr int kHpdiCtr = 16;  // workspace ints: [16] front-list count, [17] claim counter, [18] back-list count
 
 // ---------------------------------------------------------------------------
@@ -97,10 +102,9 @@ __global__ __launch_bounds__(256) void init_kernel(const uint32_t* __restrict__ 
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   // the fit kernel's queue counters (workspace, 256 B): zeroed here instead of
   // by a separate memset launch (stream order puts this before the fit kernel)
-  // -- all but the epoch, which advances by one per call (graph replays
-  // included: this kernel is the call's first node)
-  if (i < 64 && i != kWsEpoch && i != kWsEpoch + 1) ws[i] = 0;
-  if (i == 0) ++*reinterpret_cast<uint64_t*>(ws + kWsEpoch);
+  // and the ready list (one double per thread: 6 T of each)
+  if (i < 64) ws[i] = 0;
+  if (i < MDFIT_NSUBFIT * T) reinterpret_cast<double*>(reinterpret_cast<char*>(ws) + 256)[i] = 0.0;
   if (i >= MDFIT_NSUBFIT * T) return;
   const int64_t taxon = i / MDFIT_NSUBFIT;
   const int sub = (int)(i % MDFIT_NSUBFIT);  // 0 PMD-all 1 null-all 2 PMD-f 3 PMD-r 4 null-f 5 null-r
@@ -315,7 +319,6 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
   // seen this flag (no wait on a kernel that may not be running)
   if (blockIdx.x == 0 && lane == 0)
     __hip_atomic_store(ws + kWsStarted, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint64_t epoch = *reinterpret_cast<const uint64_t*>(ws + kWsEpoch);
   int mode = kIdle;
   int drained = 0, allok = 0;
   // the sub-fit of this lane's half (replicated on its lanes; for an
@@ -618,7 +621,7 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
           // arithmetic, NaN for invalid input -- as the next entry of the ready
           // list that hpdi_stream_kernel consumes beside this kernel (the
           // predictive HPDI, MDFIT-HPDI v1).  Six 8-byte agent-scope (sc1)
-          // stores by lanes 0..5 of the slot, the epoch tag last, behind the
+          // stores by lanes 0..5 of the slot, the tag last, behind the
           // wave's store wait: a reader that sees the tag sees the entry.
           auto sig = [](double v) {
             const double e = exp(-fabs(v));
@@ -639,7 +642,8 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
                                __HIP_MEMORY_SCOPE_AGENT);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           if (r == 5)
-            __hip_atomic_store(reinterpret_cast<uint64_t*>(e + 5), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(reinterpret_cast<uint64_t*>(e + 5), kReadyTag, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         }
         mode = kNextPair;
       } else if (mode == kPairFit) {
@@ -966,8 +970,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
       __builtin_amdgcn_s_sleep(8);
     }
   }
-  const uint64_t epoch =
-      __hip_atomic_load(reinterpret_cast<const uint64_t*>(ws + kWsEpoch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   HpdiIO io{};
   io.out = out;
   io.pred = pred;
@@ -998,7 +1000,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
       const double* e = ready + ei * kReadyStride;
       const uint64_t tag = __hip_atomic_load(reinterpret_cast<const uint64_t*>(e + 5), __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
-      if (tag == epoch) {
+      if (tag == kReadyTag) {
         const double q = __hip_atomic_load(e + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const double A = __hip_atomic_load(e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const double c = __hip_atomic_load(e + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1006,11 +1008,15 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
         const int64_t taxon = (int64_t)__hip_atomic_load(reinterpret_cast<const uint64_t*>(e + 4), __ATOMIC_RELAXED,
                                                          __HIP_MEMORY_SCOPE_AGENT);
         const int i = (int)(item - ei * per);
-        oitem = taxon * per + i;
-        const double N = (double)gN[taxon * kLD + i];
+        // (never out of range: K0 zeroes the list and only this call's fit
+        // kernel tags entries; a corrupt one is dropped and counted, not followed)
+        const bool sane = taxon >= 0 && taxon < T;
+        if (!sane) atomicAdd(ws + kWsBad, 1);
+        oitem = sane ? taxon * per + i : 0;
+        const double N = sane ? (double)gN[taxon * kLD + i] : 0.0;
         double lo = NAN, hi = NAN;
         bool wide = false;
-        if (N > 0.0 && !isnan(q)) {  // (the arithmetic of hpdi_prep_kernel)
+        if (sane && N > 0.0 && !isnan(q)) {  // (the arithmetic of hpdi_prep_kernel)
           const int k = i < kNHalf ? i : i - kNHalf;
           const double D = fmin(fma(A, powk(1.0 - q, k), c), 1.0);
           hpdi::WideRec rec;
@@ -1018,7 +1024,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
           if (wide) hpdi::wide_start(W, rec);
         }
         if (wide) busy = true;
-        else hpdi_write<true>(io, oitem, N, lo, hi);
+        else if (sane) hpdi_write<true>(io, oitem, N, lo, hi);
         pending = false;
         prog = true;
       }
@@ -1352,7 +1358,7 @@ int64_t mdfit_workspace_bytes(int64_t n_taxa, const mdfit_opts* opts) {
   mdfit_default_opts(&o);
   if (opts) o = *opts;
   if (o.mode == MDFIT_MODE_NUTS) return mdfit::nuts::workspace_bytes(n_taxa, o.num_samples);
-  // the 256-byte header (counters, flags, the epoch), then the ready list of
+  // the 256-byte header (counters, flags), then the ready list of
   // PMD-all modes the HPDI stream kernel consumes: 48 B per taxon
   return 256 + n_taxa * mdfit::kReadyStride * (int64_t)sizeof(double);
 }
