@@ -194,6 +194,8 @@ def test_hpdi_stream_beside_the_fit_same_record(torch_dev, monkeypatch, ppl):
         for with_pred in (True, False):
             r = engine.fit_batch_device(ty, tN, tm, opts, engine.alloc_outputs(4_000, with_pred=with_pred, opts=opts))
             torch.cuda.synchronize()
+            hdr = r.workspace[:256].view(torch.int32).cpu().numpy()
+            assert hdr[8] == 4_000 and hdr[11] == 0  # one ready entry per taxon, no corrupt entry met
             recs.append((early, with_pred, r.out.cpu().numpy()[:, :32], None if r.pred is None else r.pred.cpu().numpy(),
                          r.status.cpu().numpy()))
     base = {wp: rec for e, wp, *rec in recs if e == "0"}
