@@ -956,7 +956,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
 // streams can share a hardware queue); the late launch never waits.  Every
 // wave exits once the claim counter passes T * per.
 #ifndef MDFIT_STREAM_WAVES_PER_CU
-#define MDFIT_STREAM_WAVES_PER_CU 2
+#define MDFIT_STREAM_WAVES_PER_CU 4  // A/B at 10k and 125k taxa (tools/overlap_exp.py): 4 with the fit waves' base priority 1
 #endif
 template <bool kEarly>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPDI_WAVES_PER_EU))) void hpdi_stream_kernel(
@@ -1418,7 +1418,9 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   }
   prof_record(1, s);
   {
-    const int fit_prio = env_int("MDFIT_FIT_BASE_PRIO", 0) != 0 ? 1 : 0;
+    // fit waves above the HPDI stream's (whose waves then take the issue slots
+    // the fits leave): C2 1.42 -> 1.23 ms with 4 stream waves per CU
+    const int fit_prio = env_int("MDFIT_FIT_BASE_PRIO", 1) != 0 ? 1 : 0;
     int occ = 8;  // waves per CU the fit kernel may take: its occupancy, less the HPDI stream's
     const int cap_env = env_int("MDFIT_FIT_WAVES_PER_CU", 0);
     if (ppl == 2) {

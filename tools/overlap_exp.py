@@ -39,11 +39,10 @@ def main() -> None:
     fb = engine.alloc_outputs(a.taxa, opts=opts)
     stream = torch.cuda.current_stream()
     configs = [("default", {}), ("no_early", {"MDFIT_STREAM_WAVES_PER_CU": "0"}),
-               ("early1", {"MDFIT_STREAM_WAVES_PER_CU": "1"}), ("early3", {"MDFIT_STREAM_WAVES_PER_CU": "3"}),
-               ("early4", {"MDFIT_STREAM_WAVES_PER_CU": "4"}),
-               ("early2_fit8", {"MDFIT_STREAM_WAVES_PER_CU": "2", "MDFIT_FIT_WAVES_PER_CU": "8"}),
-               ("prio1", {"MDFIT_FIT_BASE_PRIO": "1"}),
-               ("early4_prio1", {"MDFIT_STREAM_WAVES_PER_CU": "4", "MDFIT_FIT_BASE_PRIO": "1"}),
+               ("early3", {"MDFIT_STREAM_WAVES_PER_CU": "3"}), ("early5", {"MDFIT_STREAM_WAVES_PER_CU": "5"}),
+               ("early6", {"MDFIT_STREAM_WAVES_PER_CU": "6"}),
+               ("early4_fit6", {"MDFIT_STREAM_WAVES_PER_CU": "4", "MDFIT_FIT_WAVES_PER_CU": "6"}),
+               ("early4_prio0", {"MDFIT_FIT_BASE_PRIO": "0"}),
                ("default_again", {})]
     keys = {k for _, e in configs for k in e}
     ref = None
