@@ -192,7 +192,7 @@ constexpr unsigned kEscIndef = 1u, kEscProbe = 2u, kEscNc = 4u, kEscExhOk = 8u, 
 struct HpdiIO {
   // kFit
   const uint32_t* gN;
-  const double* theta;  // PMD-all (q, A, c, phi) per taxon (K3a)
+  const double* ready;  // the ready list of PMD-all modes (fit_kernel; complete when K4a runs)
   double* out;
   float* pred;
   int per;  // positions per taxon written (30, or 1 without pred)
@@ -866,12 +866,17 @@ __global__ __launch_bounds__(kWave) void hpdi_prep_kernel(HpdiIO io, int64_t n_i
   const bool valid = item < n_items;
   double N = 0.0, a = 0.0, b = 0.0;
   bool skip = true;
+  int64_t oitem = item;  // the output index (kFit: taxon * per + position)
   if (valid) {
     if (kFit) {
-      const int64_t t = item / io.per;
-      const int i = (int)(item - t * io.per);
-      const double* dg = io.theta + t * 4;  // PMD-all: (q, A, c, phi)
+      // items in ready-list order: entry item / per, stream-ordered after the
+      // fit kernel (every entry written)
+      const int64_t ei = item / io.per;
+      const int i = (int)(item - ei * io.per);
+      const double* dg = io.ready + ei * kReadyStride;  // PMD-all: (q, A, c, phi, taxon, tag)
       const double q = dg[0], A = dg[1], c = dg[2], phi = dg[3];
+      const int64_t t = (int64_t)__double_as_longlong(dg[4]);
+      oitem = t * io.per + i;
       N = (double)io.gN[t * kLD + i];
       if (N > 0.0 && !isnan(q)) {
         const int k = i < kNHalf ? i : i - kNHalf;
@@ -887,7 +892,7 @@ __global__ __launch_bounds__(kWave) void hpdi_prep_kernel(HpdiIO io, int64_t n_i
       skip = !(N > 0.0);
     }
   }
-  hpdi_position<kFit>(io, item, valid, skip, N, a, b, n_items, ctr, recs);
+  hpdi_position<kFit>(io, oitem, valid, skip, N, a, b, n_items, ctr, recs);
 }
 
 // one lane per wide window at a time: every trip each busy lane runs one level
@@ -975,7 +980,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
   io.pred = pred;
   io.per = per;
   const int64_t n_items = T * per;
-  hpdi::Wide W;
+  // a lane's wide-window state lives in LDS between trips (~300 B per lane): in
+  // registers it stays live through the item set-up (prep_position) of the
+  // other lanes and the kernel spilled
+  __shared__ hpdi::Wide sW[kWave];
+  hpdi::Wide& W = sW[lane];
   int64_t item = 0, oitem = 0;  // the claimed item; its output index taxon * per + position
   bool busy = false, pending = false, drained = false;
   while (true) {
@@ -1223,6 +1232,11 @@ double* ready_buf(void* ws) { return reinterpret_cast<double*>(static_cast<char*
 mdfit::hpdi::WideRec* hpdi_recs(void* ws) {
   return reinterpret_cast<mdfit::hpdi::WideRec*>(static_cast<char*>(ws) + 256);
 }
+// (the fit's K4a / K4b path from kPpl2MinTaxa taxa: after the ready list)
+mdfit::hpdi::WideRec* hpdi_recs_after_ready(void* ws, int64_t n_taxa) {
+  return reinterpret_cast<mdfit::hpdi::WideRec*>(static_cast<char*>(ws) + 256 +
+                                                 n_taxa * mdfit::kReadyStride * (int64_t)sizeof(double));
+}
 
 // The side streams of mdfit_fit_batch's forks -- [0] the HPDI stream kernel
 // beside the fit kernel, [1] the record assembly beside the late HPDI launch --
@@ -1359,8 +1373,10 @@ int64_t mdfit_workspace_bytes(int64_t n_taxa, const mdfit_opts* opts) {
   if (opts) o = *opts;
   if (o.mode == MDFIT_MODE_NUTS) return mdfit::nuts::workspace_bytes(n_taxa, o.num_samples);
   // the 256-byte header (counters, flags), then the ready list of
-  // PMD-all modes the HPDI stream kernel consumes: 48 B per taxon
-  return 256 + n_taxa * mdfit::kReadyStride * (int64_t)sizeof(double);
+  // PMD-all modes (48 B per taxon); from kPpl2MinTaxa taxa (the HPDI after the
+  // fit, K4a -> K4b) room for every position's wide-window record
+  return 256 + n_taxa * mdfit::kReadyStride * (int64_t)sizeof(double) +
+         (n_taxa >= kPpl2MinTaxa ? n_taxa * mdfit::kNPos * (int64_t)sizeof(mdfit::hpdi::WideRec) : 0);
 }
 
 int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t n_taxa,
@@ -1408,7 +1424,15 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   // K4 (early): the predictive HPDI streamed beside the fit kernel, on side
   // stream 0 from after K0; its grid -- MDFIT_STREAM_WAVES_PER_CU waves per CU
   // -- is the room the fit kernel's grid leaves
-  const int early_per_cu = fk != nullptr ? env_int("MDFIT_STREAM_WAVES_PER_CU", MDFIT_STREAM_WAVES_PER_CU) : 0;
+  // The HPDI streams beside the fit below kPpl2MinTaxa taxa -- the regime where
+  // the call is bounded by the fit kernel's tail, which the stream fills --
+  // and runs after the fit from there (the fit kernel fills the chip by itself;
+  // K4a -> K4b at full occupancy, longest windows first).  MDFIT_HPDI_STREAM=1
+  // streams at any size (A/B; the workspace has no wide-window list below).
+  bool stream = n_taxa < kPpl2MinTaxa;
+  if (const char* e = std::getenv("MDFIT_HPDI_STREAM")) stream = stream || std::atoi(e) != 0;
+  const int early_per_cu =
+      (fk != nullptr && stream) ? env_int("MDFIT_STREAM_WAVES_PER_CU", MDFIT_STREAM_WAVES_PER_CU) : 0;
   ForkScope fork_hp(early_per_cu > 0 ? fk : nullptr, s, 0);
   if (early_per_cu > 0) {
     const int64_t g = fit_grid(mdfit::hpdi_stream_kernel<true>, n_items, mdfit::kWave, early_per_cu);
@@ -1447,12 +1471,21 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   hipLaunchKernelGGL(mdfit::assemble_kernel, dim3((unsigned)n_taxa), dim3(mdfit::kWave), 0, fork_as.side(), y, N,
                      mm, n_taxa, out, pred, status);
   if (int rc = check_launch("assemble_kernel")) return rc;
-  {
+  if (stream) {
     const int64_t g = fit_grid(mdfit::hpdi_stream_kernel<false>, n_items, mdfit::kWave,
                                env_int("MDFIT_HPDI_WAVES_PER_CU", 0));
     hipLaunchKernelGGL(mdfit::hpdi_stream_kernel<false>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, N, n_taxa, per,
                        out, pred, ws, (const double*)ready);
     if (int rc = check_launch("hpdi_stream_kernel")) return rc;
+  } else {
+    mdfit::HpdiIO io{};
+    io.gN = N;
+    io.ready = ready;
+    io.out = out;
+    io.pred = pred;
+    io.per = per;
+    if (int rc = launch_hpdi<true>(io, n_items, ws + mdfit::kHpdiCtr, hpdi_recs_after_ready(workspace, n_taxa), s))
+      return rc;
   }
   if (int rc = fork_as.join()) return rc;
   if (int rc = fork_hp.join()) return rc;
