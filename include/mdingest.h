@@ -111,6 +111,16 @@ int mdi_codes(int64_t n_keep, const int64_t* perm, int n_cols, const int32_t* co
               int n_threads, int32_t* const* out, uint8_t* const* used);
 int mdi_remap(int64_t n, int n_cols, int32_t* const* codes, const int32_t* const* remap, int n_threads);
 
+/* mdi_first_index / mdi_interleave: the packing of group_to_numpyro_data
+ * (fits.py:398-419) for fits.pack_counts.  mdi_first_index numbers the
+ * categories of codes[n] (< n_cat) in first-appearance order (pd.factorize):
+ * taxon[i] = that number, first[t] = the first row of taxon t; returns the
+ * number of taxa T (first holds n entries at most), -1 on a bad code.
+ * mdi_interleave writes out[i][c] = cols[c][i] (n rows, n_cols <= 64 uint32
+ * columns: the [T][30][12] mismatch block), parallel over row ranges. */
+int64_t mdi_first_index(int64_t n, const int32_t* codes, int32_t n_cat, int64_t* taxon, int64_t* first);
+int mdi_interleave(int64_t n, int n_cols, const uint32_t* const* cols, uint32_t* out, int n_threads);
+
 /* Worker threads the library uses when a call passes n_threads <= 0: the
  * process's CPU share -- OMP_NUM_THREADS when set (a GPU box grants 16 cores
  * per GPU and sets it), else the CPUs of the affinity mask -- never the whole

@@ -299,6 +299,42 @@ int mdi_remap(int64_t n, int n_cols, int32_t* const* codes, const int32_t* const
   return 0;
 }
 
+int64_t mdi_first_index(int64_t n, const int32_t* codes, int32_t n_cat, int64_t* taxon, int64_t* first) {
+  if (n < 0 || n_cat < 0 || (n > 0 && (!codes || !taxon || !first))) return arg_error("mdi_first_index: bad arguments");
+  std::vector<int64_t> index((size_t)n_cat, -1);
+  int64_t T = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t k = codes[i];
+    if (k < 0 || k >= n_cat) return arg_error("mdi_first_index: code out of its table");
+    int64_t& t = index[(size_t)k];
+    if (t < 0) {
+      t = T;
+      first[T++] = i;
+    }
+    taxon[i] = t;
+  }
+  return T;
+}
+
+int mdi_interleave(int64_t n, int n_cols, const uint32_t* const* cols, uint32_t* out, int n_threads) {
+  if (n < 0 || n_cols < 1 || n_cols > 64 || (n > 0 && (!cols || !out))) return arg_error("mdi_interleave: bad arguments");
+  for (int c = 0; c < n_cols; ++c)
+    if (n > 0 && !cols[c]) return arg_error("mdi_interleave: bad column");
+  // row blocks of 2048: the block's slices of every column stay in L1/L2
+  // while the interleaved rows are written out sequentially
+  for_ranges(pool_size(n_threads, n), n, [&](int, int64_t lo, int64_t hi) {
+    for (int64_t a = lo; a < hi; a += 2048) {
+      const int64_t b = std::min<int64_t>(hi, a + 2048);
+      for (int c = 0; c < n_cols; ++c) {
+        const uint32_t* src = cols[c];
+        uint32_t* dst = out + c;
+        for (int64_t i = a; i < b; ++i) dst[i * n_cols] = src[i];
+      }
+    }
+  });
+  return 0;
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------

@@ -64,8 +64,37 @@ def _load():
         lib.mdi_remap.restype = ctypes.c_int
         lib.mdi_noise.argtypes = [vp, i64, ctypes.c_int, vp]
         lib.mdi_noise.restype = ctypes.c_int
+        lib.mdi_first_index.argtypes = [i64, vp, ctypes.c_int32, vp, vp]
+        lib.mdi_first_index.restype = i64
+        lib.mdi_interleave.argtypes = [i64, ctypes.c_int, vp, vp, ctypes.c_int]
+        lib.mdi_interleave.restype = ctypes.c_int
         _LIB = lib
     return _LIB
+
+
+def first_index(codes: np.ndarray, n_cat: int):
+    """pd.factorize of category codes (first-appearance numbering), natively
+    (mdi_first_index): (taxon int64[n], first int64[T])."""
+    codes = np.ascontiguousarray(codes, dtype=np.int32)
+    n = codes.size
+    taxon = np.empty(n, np.int64)
+    first = np.empty(n, np.int64)
+    T = _load().mdi_first_index(n, codes.ctypes.data, int(n_cat), taxon.ctypes.data, first.ctypes.data)
+    if T < 0:
+        raise ValueError(_load().mdi_counts_error().decode())
+    return taxon, first[:T]
+
+
+def interleave(cols, out2d: np.ndarray, n_threads: int = 0) -> None:
+    """out2d[:, j] = cols[j] for uint32 columns (mdi_interleave)."""
+    cols = [np.ascontiguousarray(c, dtype=np.uint32) for c in cols]
+    n = out2d.shape[0]
+    if out2d.dtype != np.uint32 or not out2d.flags.c_contiguous or out2d.shape[1] != len(cols) or \
+            any(c.shape != (n,) for c in cols):
+        raise ValueError("interleave: shapes / dtypes")
+    ptrs = (ctypes.c_void_p * len(cols))(*[c.ctypes.data for c in cols])
+    if _load().mdi_interleave(n, len(cols), ptrs, out2d.ctypes.data, int(n_threads)) != 0:
+        raise ValueError(_load().mdi_counts_error().decode())
 
 
 def noise(mm: np.ndarray, n_threads: int = 0) -> np.ndarray:

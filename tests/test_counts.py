@@ -69,6 +69,29 @@ def test_top_max_fits_matches_reference(ref_meta):
             assert got == expect, (name, k)
 
 
+@pytest.mark.parametrize("sorted_cats", [True, False])
+def test_top_max_fits_fast_path_equals_groupby(sorted_cats):
+    """The bincount selection picks nlargest(keep="first")'s set on tied sums
+    and unsorted / unobserved categories, and returns the table itself when
+    every taxon is selected."""
+    rng = np.random.default_rng(5)
+    n = 4000
+    cats = np.arange(300) * 7 + 11
+    if not sorted_cats:
+        cats = rng.permutation(cats)
+    codes = rng.integers(0, 250, n)  # categories 250.. never observed
+    df = pd.DataFrame({"tax_id": pd.Categorical.from_codes(codes, categories=cats),
+                       "N_alignments": rng.integers(1, 4, n), "x": np.arange(n)})
+    n_taxa = len(np.unique(codes))
+    for k in [1, 2, 17, 100, n_taxa - 1]:
+        top = df.groupby("tax_id", observed=True)["N_alignments"].sum().nlargest(k).index
+        want = df[df["tax_id"].isin(top)]
+        got = fits.extract_top_max_fits(df, k)
+        assert got.index.equals(want.index), k
+    assert fits.extract_top_max_fits(df, n_taxa) is df
+    assert fits.extract_top_max_fits(df, n_taxa + 5) is df
+
+
 def test_cut_semantics_are_frozen(tmp_path):
     """N_alignments >= min_alignments AND y_sum_total >= min_y_sum (counts.py:207-209),
     y_sum_total = sum of the forward substitution at z > 0 + reverse at z < 0."""

@@ -130,6 +130,7 @@ def main() -> None:
     ap.add_argument("--dir", default="/tmp/mdfit_c5")
     ap.add_argument("--stages", type=int, default=2, help="files to time stage by stage first (0: none)")
     ap.add_argument("--gen-procs", type=int, default=8)
+    ap.add_argument("--readers", type=int, default=0, help="files read ahead (main.N_READERS; 0: its default)")
     ap.add_argument("--trace", action="store_true", help="print the per-thread stage timeline of the driver run")
     a = ap.parse_args()
     import torch
@@ -163,6 +164,8 @@ def main() -> None:
         stages(files[: a.stages], d / "out_stages", a.inference)
     cfg = _cfg(d / "out", a.inference)
     cfg.add_filenames(files)
+    if a.readers:
+        driver.N_READERS = a.readers
     if world > 1:
         dist.barrier()
     events = _trace_wrappers() if a.trace else None
