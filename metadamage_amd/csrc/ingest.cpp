@@ -86,8 +86,11 @@ namespace {
 
 // The scanners below take no end pointer: every line they see ends in '\n'
 // (parse_chunk hands a last line without one over as a copy with it appended),
-// and none of them moves past a '\n', so the newline is the sentinel.
-inline bool parse_int(const char*& p, int64_t* v) {
+// and none of them moves past a '\n', so the newline is the sentinel.  lim
+// bounds the bytes that may be READ (the mapping, or the padded copy): an
+// integer with 8 readable bytes ahead is converted 8 digits at a time (SWAR),
+// which spares the digit loop's branch per digit and its mispredicted exit.
+inline bool parse_int(const char*& p, const char* lim, int64_t* v) {
   bool neg = false;
   if (*p == '-' || *p == '+') {
     neg = *p == '-';
@@ -95,9 +98,32 @@ inline bool parse_int(const char*& p, int64_t* v) {
   }
   const char* s = p;
   int64_t x = 0;
-  while ((unsigned)(*p - '0') < 10u) {
-    x = x * 10 + (*p - '0');
-    ++p;
+  if (lim - p >= 8) {
+    uint64_t w;
+    std::memcpy(&w, p, 8);
+    const uint64_t t = w ^ 0x3030303030303030ull;  // digits -> 0..9
+    // a byte is a non-digit iff its high nibble is set, or adding 6 sets it
+    // (carries only leave the first non-digit byte, upward: never read)
+    const uint64_t nd = (t | (t + 0x0606060606060606ull)) & 0xF0F0F0F0F0F0F0F0ull;
+    const int len = nd ? __builtin_ctzll(nd) >> 3 : 8;
+    if (len > 0) {
+      uint64_t y = t << (8 * (8 - len));  // the len digits right-aligned, first digit most significant
+      y = (y * 10 + (y >> 8)) & 0x00FF00FF00FF00FFull;
+      y = (y * 100 + (y >> 16)) & 0x0000FFFF0000FFFFull;
+      y = (y * 10000 + (y >> 32)) & 0xFFFFFFFFull;
+      x = (int64_t)y;
+      p += len;
+    }
+    if (len == 8)
+      while ((unsigned)(*p - '0') < 10u) {
+        x = x * 10 + (*p - '0');
+        ++p;
+      }
+  } else {
+    while ((unsigned)(*p - '0') < 10u) {
+      x = x * 10 + (*p - '0');
+      ++p;
+    }
   }
   if (p == s) return false;
   if (*p == '.') {  // tolerate a float rendering of an integer ("12.0")
@@ -113,6 +139,20 @@ inline std::string_view field(const char*& p) {
   const char* s = p;
   while (*p != '\t' && *p != '\n' && *p != '\r') ++p;
   return std::string_view(s, (size_t)(p - s));
+}
+
+// a string field, interned: a row repeating the previous row's value (a
+// taxon's 30 rows) is matched in place without scanning for its end
+inline int32_t intern(const char*& p, const char* lim, LocalStrings& ls) {
+  const size_t n = ls.last.size();
+  if (ls.last_id >= 0 && (size_t)(lim - p) > n && std::memcmp(p, ls.last.data(), n) == 0) {
+    const char d = p[n];
+    if (d == '\t' || d == '\n' || d == '\r') {
+      p += n;
+      return ls.last_id;
+    }
+  }
+  return ls.add(field(p));
 }
 
 inline bool tab(const char*& p) {
@@ -138,33 +178,37 @@ struct Out {
   int64_t *tax_id, *nal, *pos, *counts;
   int32_t* code[3];
   int64_t rows;
+  const char* map_end;  // readable bytes of the mapping end here
 };
 
 // one line [p, its '\n'] into row r; false on a malformed field (col set)
-inline bool parse_line(const char*& p, int format, const Out& o, Chunk* c, int64_t r, int& col) {
+inline bool parse_line(const char*& p, const char* lim, int format, const Out& o, Chunk* c, int64_t r, int& col) {
   col = 0;
   int64_t tid, nal, pos;
-  std::string_view name, rank;
-  if (!parse_int(p, &tid) || !tab(p)) return false;
+  int32_t name = 0, rank = 0;
+  if (!parse_int(p, lim, &tid) || !tab(p)) return false;
   ++col;
   if (format == 22) {
-    name = field(p);
+    name = intern(p, lim, c->str[MDI_STR_NAME]);
     if (!tab(p)) return false;
     ++col;
-    rank = field(p);
+    rank = intern(p, lim, c->str[MDI_STR_RANK]);
     if (!tab(p)) return false;
     ++col;
+  } else {  // the 20-column table has no name / rank: every row interns ""
+    name = c->str[MDI_STR_NAME].add(std::string_view());
+    rank = c->str[MDI_STR_RANK].add(std::string_view());
   }
-  if (!parse_int(p, &nal) || !tab(p)) return false;
+  if (!parse_int(p, lim, &nal) || !tab(p)) return false;
   ++col;
-  const std::string_view strand = field(p);
+  const int32_t strand = intern(p, lim, c->str[MDI_STR_STRAND]);
   if (!tab(p)) return false;
   ++col;
-  if (!parse_int(p, &pos)) return false;
+  if (!parse_int(p, lim, &pos)) return false;
   ++col;
   for (int j = 0; j < 16; ++j) {  // column-major: counts[j][rows]
     int64_t v;
-    if (!tab(p) || !parse_int(p, &v)) return false;
+    if (!tab(p) || !parse_int(p, lim, &v)) return false;
     o.counts[(int64_t)j * o.rows + r] = v;
     ++col;
   }
@@ -174,9 +218,9 @@ inline bool parse_line(const char*& p, int format, const Out& o, Chunk* c, int64
   o.tax_id[r] = tid;
   o.nal[r] = nal;
   o.pos[r] = pos;
-  o.code[MDI_STR_NAME][r] = c->str[MDI_STR_NAME].add(name);
-  o.code[MDI_STR_RANK][r] = c->str[MDI_STR_RANK].add(rank);
-  o.code[MDI_STR_STRAND][r] = c->str[MDI_STR_STRAND].add(strand);
+  o.code[MDI_STR_NAME][r] = name;
+  o.code[MDI_STR_RANK][r] = rank;
+  o.code[MDI_STR_STRAND][r] = strand;
   return true;
 }
 
@@ -188,12 +232,15 @@ void parse_chunk(Chunk* c, int format, const Out& o) {
   // a last line without its newline: parsed from a copy that has one (its
   // string fields then view the copy, which lives as long as the chunk)
   const char* tail = end;
+  size_t tail_len = 0;
   if (end > p && end[-1] != '\n') {
     const char* q = end;
     while (q > p && q[-1] != '\n') --q;
     tail = q;
     c->tail.assign(q, (size_t)(end - q));
     c->tail.push_back('\n');
+    tail_len = c->tail.size();
+    c->tail.append(8, '\0');  // readable padding for parse_int's 8-byte loads
   }
   int col = 0;
   auto bad = [&](int colno) {
@@ -203,14 +250,15 @@ void parse_chunk(Chunk* c, int format, const Out& o) {
   };
   for (int part = 0; part < 2; ++part) {
     const char* q = part == 0 ? p : c->tail.data();
-    const char* qe = part == 0 ? tail : c->tail.data() + c->tail.size();
+    const char* qe = part == 0 ? tail : c->tail.data() + tail_len;
+    const char* lim = part == 0 ? o.map_end : c->tail.data() + c->tail.size();
     while (q < qe) {
       if (*q == '\n' || *q == '\r') {  // blank line
         ++q;
         continue;
       }
       if (r >= rend) return bad(0);  // (rows were counted on the same bytes)
-      if (!parse_line(q, format, o, c, r, col)) return bad(col);
+      if (!parse_line(q, lim, format, o, c, r, col)) return bad(col);
       ++r;
     }
     if (c->tail.empty()) break;
@@ -319,7 +367,8 @@ int mdi_parse_into(mdi_table* t, int64_t* tax_id, int64_t* n_alignments, int64_t
   if (!t || !tax_id || !n_alignments || !position || !counts16 || !name_code || !rank_code || !strand_code)
     return fail(MDI_E_ARG, "null argument");
   if (t->parsed) return fail(MDI_E_ARG, "table already parsed");
-  const Out o{tax_id, n_alignments, position, counts16, {name_code, rank_code, strand_code}, t->rows};
+  const Out o{tax_id, n_alignments, position, counts16, {name_code, rank_code, strand_code}, t->rows,
+              (const char*)t->map + t->size};
   const int format = t->format;
   parallel_chunks(t->chunks, [&](size_t i) { parse_chunk(&t->chunks[i], format, o); });
   for (const Chunk& c : t->chunks)

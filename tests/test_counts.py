@@ -201,6 +201,43 @@ def test_native_reader_errors(tmp_path):
         ingest.read_table(f)
 
 
+@pytest.mark.parametrize("newline_at_end", [True, False])
+def test_native_reader_integer_widths(tmp_path, newline_at_end):
+    """The 8-digits-at-a-time integer scan: every width 1..18, signs, "12.0",
+    names that only share a prefix with the previous row's, and a last field
+    within 8 bytes of the end of the file (read with the byte-wise scan)."""
+    from metadamage_amd import ingest
+
+    rng = np.random.default_rng(3)
+    rows, want = [], []
+    names = ["taxon_a", "taxon_ab", "taxon_a", "taxon_", "x"]
+    for i in range(400):
+        w = 1 + i % 18
+        v = [int(rng.integers(10 ** (w - 1) if w > 1 else 0, 10 ** w)) for _ in range(16)]
+        pos = int(rng.integers(0, 15))
+        nal = int(rng.integers(0, 10 ** (1 + i % 12)))
+        tid = int(rng.integers(1, 10 ** (1 + i % 17)))
+        sv = [str(x) for x in v]
+        if i % 7 == 0:
+            sv[3] = f"+{v[3]}"
+        if i % 11 == 0:
+            sv[5] = f"{v[5]}.000"
+        rows.append("\t".join([str(tid), names[i % 5], "species", str(nal), "5'" if i % 2 else "3'", str(pos), *sv]))
+        want.append((tid, names[i % 5], nal, pos, v))
+    rows.append("\t".join(["5", "x", "genus", "1", "5'", "-3"] + ["1"] * 15 + ["7"]))
+    want.append((5, "x", 1, -3, [1] * 15 + [7]))
+    f = tmp_path / "w.tsv"
+    f.write_text("\n".join(rows) + ("\n" if newline_at_end else ""))
+    for nt in (1, 3):
+        t = ingest.read_table(f, nt)
+        assert t.rows == len(want)
+        assert list(t.tax_id) == [w[0] for w in want]
+        assert list(t.names[t.name_code]) == [w[1] for w in want]
+        assert list(t.n_alignments) == [w[2] for w in want]
+        assert list(t.position) == [w[3] for w in want]
+        assert np.array_equal(t.counts.T, np.array([w[4] for w in want], dtype=np.int64))
+
+
 def test_native_reader_on_the_shipped_headed_files():
     from metadamage_amd import ingest
 

@@ -87,7 +87,7 @@ def _trace_wrappers():
     the per-thread busy time and the critical path of main.main()."""
     import threading
 
-    from metadamage_amd import counts, fits, io
+    from metadamage_amd import counts, fits, ingest, io
 
     events = []
 
@@ -109,6 +109,10 @@ def _trace_wrappers():
     wrap(fits, "make_df_fit_results", "frame_results")
     wrap(fits, "make_df_fit_predictions", "frame_predictions")
     wrap(io.Parquet, "save", "parquet")
+    wrap(fits, "get_fits", "get_fits")
+    wrap(fits, "get_top_max_fits", "top_n")
+    wrap(ingest, "noise", "noise")
+    wrap(ingest, "read_table", "parse")
     return events
 
 
