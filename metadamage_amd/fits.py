@@ -335,18 +335,39 @@ CACHE_KEYS = ["min_alignments", "min_y_sum", "substitution_bases_forward", "subs
               "N_fits", "shortname", "filename", "inference"]
 
 
-def get_fits(df_counts, cfg, opts=None, shard=True, writer=None):
+def _cache_hit(cfg) -> bool:
+    """This rank's fit cache check (fits.py:767-783): both parquets exist (and
+    --forced is off) with metadata equal on CACHE_KEYS."""
+    parquet_fit_results = io.Parquet(cfg.filename_fit_results)
+    parquet_fit_predictions = io.Parquet(cfg.filename_fit_predictions)
+    if not (parquet_fit_results.exists(cfg.forced) and parquet_fit_predictions.exists(cfg.forced)):
+        return False
+    metadata_cfg = cfg.to_dict()
+    return utils.metadata_is_similar(parquet_fit_results.load_metadata(), metadata_cfg, include=CACHE_KEYS) and \
+        utils.metadata_is_similar(parquet_fit_predictions.load_metadata(), metadata_cfg, include=CACHE_KEYS)
+
+
+def prepare_fits(df_counts, cfg):
+    """The host work of get_fits ahead of the device call -- the top-N cut and
+    the packing -- for a reader thread (main.main runs it beside the previous
+    file's fit); None when this rank's fit cache is a hit (get_fits decides)."""
+    if _cache_hit(cfg):
+        return None
+    return pack_counts(get_top_max_fits(df_counts, cfg.N_fits), cfg)
+
+
+def get_fits(df_counts, cfg, opts=None, shard=True, writer=None, packed=None, deferred=False):
     """fits.py:754-807.  shard: split the taxa over the torch.distributed ranks
-    (rank 0 gathers and saves); writer: an executor for the parquet saves."""
+    (rank 0 gathers and saves); writer: an executor for the parquet saves;
+    packed: prepare_fits(df_counts, cfg) when it ran already.  deferred: return
+    a callable that builds the two frames and submits their saves (main.main
+    runs it on a writer thread while the next file fits) instead of the
+    frames, once the device results are on the host."""
     from .distributed import all_ranks_agree
 
     parquet_fit_results = io.Parquet(cfg.filename_fit_results)
     parquet_fit_predictions = io.Parquet(cfg.filename_fit_predictions)
-    hit = False
-    if parquet_fit_results.exists(cfg.forced) and parquet_fit_predictions.exists(cfg.forced):
-        metadata_cfg = cfg.to_dict()
-        hit = utils.metadata_is_similar(parquet_fit_results.load_metadata(), metadata_cfg, include=CACHE_KEYS) and \
-            utils.metadata_is_similar(parquet_fit_predictions.load_metadata(), metadata_cfg, include=CACHE_KEYS)
+    hit = _cache_hit(cfg)
     if shard:  # a taxon-sharded fit is collective: every rank reuses the cache or none does
         hit = all_ranks_agree(hit)
     if hit:
@@ -355,14 +376,24 @@ def get_fits(df_counts, cfg, opts=None, shard=True, writer=None):
         logger.info("Fit: Loading fits from parquet-file.")
         return parquet_fit_results.load(), parquet_fit_predictions.load()
     logger.info("Fit: Generating fits and saving to file.")
-    df_counts_top_N = get_top_max_fits(df_counts, cfg.N_fits)
+    p = packed if packed is not None else pack_counts(get_top_max_fits(df_counts, cfg.N_fits), cfg)
     # fits.py:792-799
     mcmc_kwargs = dict(progress_bar=False, num_warmup=500, num_samples=1000, num_chains=1, chain_method="sequential")
-    df_fit_results, df_fit_predictions = compute_fits(df_counts_top_N, cfg, mcmc_kwargs, opts=opts, shard=shard)
-    if df_fit_results is None:
+    res = fit_packed(p, opts if opts is not None else make_opts(cfg, mcmc_kwargs), shard=shard)
+    if res is None:  # non-zero rank of a multi-GPU job
         return None, None
-    from .counts import _save
+    out, pred, status = res
+    keep = status == _lib.OK
+    for t in np.where(~keep)[0]:
+        logger.warning(f"Fit: tax_id {p.tax_id[t]} failed (status {int(status[t])}). Skipping.")
 
-    _save(writer, parquet_fit_results, df_fit_results, cfg.to_dict())
-    _save(writer, parquet_fit_predictions, df_fit_predictions, cfg.to_dict())
-    return df_fit_results, df_fit_predictions
+    def finish():
+        from .counts import _save
+
+        df_fit_results = make_df_fit_results(p, out, keep, cfg)
+        df_fit_predictions = make_df_fit_predictions(p, pred, keep, cfg)
+        _save(writer, parquet_fit_results, df_fit_results, cfg.to_dict())
+        _save(writer, parquet_fit_predictions, df_fit_predictions, cfg.to_dict())
+        return df_fit_results, df_fit_predictions
+
+    return finish if deferred else finish()

@@ -5,8 +5,8 @@ frozen cuts, then get_fits.  The reference ran the files one after another and
 dispatched each file's fits to a process pool; here
 
   * the stages of consecutive files overlap: reader threads ingest files
-    i+1 and i+2 (the native reader releases the GIL) while file i is packed
-    and fitted, and the parquet writes (counts, fit_results, fit_predictions) run
+    i+1 and i+2 and pack them for the fit (the native reader releases the
+    GIL) while file i is fitted, and the parquet writes (counts, fit_results, fit_predictions) run
     on writer threads (pyarrow releases the GIL while encoding);
   * in a multi-GPU job (torch.distributed initialised) with at least as many
     files as ranks, whole files are dealt round-robin to the ranks and each
@@ -20,7 +20,7 @@ from __future__ import annotations
 import copy
 import logging
 from collections import deque
-from concurrent.futures import ThreadPoolExecutor
+from concurrent.futures import Future, ThreadPoolExecutor
 
 from . import counts, fits, utils
 
@@ -61,9 +61,13 @@ class _Writer:
 
 
 def _load(filename, cfg, writer, save=True):
+    """Reader thread: the counts table of one file, then the host work of its
+    fit ahead of the device call (fits.prepare_fits: top-N, packing)."""
     cfg_f = copy.copy(cfg)
     cfg_f.add_filename(filename)
-    return cfg_f, counts.load_counts(cfg_f, writer=writer, save=save)
+    df_counts = counts.load_counts(cfg_f, writer=writer, save=save)
+    packed = fits.prepare_fits(df_counts, cfg_f) if len(df_counts) > 0 else None
+    return cfg_f, df_counts, packed
 
 
 def main(filenames, cfg, opts=None):
@@ -85,7 +89,7 @@ def main(filenames, cfg, opts=None):
         writer = _Writer(pool)
         ahead = deque(reader.submit(_load, f, cfg, writer, save) for f in mine[:N_READERS])
         for i in range(len(mine)):
-            cfg_f, df_counts = ahead.popleft().result()
+            cfg_f, df_counts, packed = ahead.popleft().result()
             if i + N_READERS < len(mine):
                 ahead.append(reader.submit(_load, mine[i + N_READERS], cfg, writer, save))
             cfg.add_filename(cfg_f.filename)  # the caller's cfg follows the files as in the reference
@@ -97,8 +101,12 @@ def main(filenames, cfg, opts=None):
                 accepted = all_ranks_agree(accepted)
             if not accepted:
                 continue
-            results[cfg_f.shortname] = fits.get_fits(df_counts, cfg_f, opts=opts, shard=not shard_files,
-                                                     writer=writer)
+            r = fits.get_fits(df_counts, cfg_f, opts=opts, shard=not shard_files, writer=writer, packed=packed,
+                              deferred=True)
+            # the frames are built (and their saves submitted) on a writer
+            # thread while the next file fits
+            results[cfg_f.shortname] = pool.submit(r) if callable(r) else r
             logger.debug("End of loop\n")
+        results = {k: (v.result() if isinstance(v, Future) else v) for k, v in results.items()}
         writer.drain()
     return results

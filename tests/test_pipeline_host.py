@@ -78,8 +78,12 @@ def _files(tmp_path, n):
 
 
 def _fake_get_fits(log):
-    def get_fits(df_counts, cfg, opts=None, shard=True, writer=None):
+    def get_fits(df_counts, cfg, opts=None, shard=True, writer=None, packed=None, deferred=False):
         log.append((cfg.shortname, shard, len(df_counts)))
+        # the reader thread packed the file (every taxon: max_fits unset)
+        assert packed is not None and packed.n_taxa == df_counts["tax_id"].nunique()
+        if deferred:
+            return lambda: (cfg.shortname, shard)
         return cfg.shortname, shard
     return get_fits
 
@@ -91,6 +95,7 @@ def test_main_overlaps_reads_and_writes(tmp_path, monkeypatch):
     cfg = _cfg(tmp_path / "out")
     res = main_mod.main(files, cfg)
     assert list(res) == ["sample0", "sample1", "sample2"]
+    assert res["sample1"] == ("sample1", True)  # the deferred frames resolved
     assert [s for s, _, _ in log] == ["sample0", "sample1", "sample2"] and all(sh for _, sh, _ in log)
     assert cfg.shortname == "sample2"  # the caller's cfg follows the files
     for f in files:  # the counts parquet written on the writer threads is the computed table
