@@ -68,12 +68,15 @@ const char* mdi_last_error(void);
  * y_sum_total[r] = that taxon's substitution-count sum, and perm[0..n) = the
  * kept rows (N_alignments >= min_alignments, y_sum_total >= min_y_sum) in
  * N_alignments, tax_id, z order (all descending, ties in file order).
- * Returns n (>= 0) or a negative MDI_E_* code.  taxon, y_sum_total and perm
- * hold `rows` entries. */
+ * uniq (nullable, `rows` entries) receives the tax_id of each taxon index and
+ * n_taxa (nullable) their number.  Parallel over row ranges (n_threads <= 0:
+ * mdi_default_threads()).  Returns n (>= 0) or a negative MDI_E_* code.
+ * taxon, y_sum_total and perm hold `rows` entries. */
 int64_t mdi_select(int64_t rows, const int64_t* tax_id, const int64_t* n_alignments, const int64_t* position,
                    const int64_t* counts16, const int32_t* strand_code, const uint8_t* code_is_fwd,
                    int32_t n_codes, const char* sub_fwd, const char* sub_rev, int64_t min_alignments,
-                   int64_t min_y_sum, int32_t* taxon, int64_t* y_sum_total, int64_t* perm);
+                   int64_t min_y_sum, int n_threads, int32_t* taxon, int64_t* y_sum_total, int64_t* perm,
+                   int64_t* uniq, int64_t* n_taxa);
 
 /* mdi_gather writes the numeric columns of the counts table for the rows
  * perm[0..n_keep), downcast as utils.py:329-356 (add_reference_counts,

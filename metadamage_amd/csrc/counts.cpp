@@ -62,6 +62,25 @@ double order_key(int64_t p) { return p > 0 ? 1.0 / (double)p : (double)p; }
 
 thread_local char g_cerr[256] = "";
 
+int pool_size(int n_threads, int64_t n) {
+  int nt = n_threads > 0 ? n_threads : mdi_default_threads();
+  if (nt < 1) nt = 1;
+  if (n < (int64_t)nt * 65536) nt = (int)std::max<int64_t>(1, n / 65536);
+  return nt > 64 ? 64 : nt;
+}
+
+template <typename F>
+void for_ranges(int nt, int64_t n, F f) {
+  if (nt <= 1) {
+    f(0, (int64_t)0, n);
+    return;
+  }
+  std::vector<std::thread> pool;
+  for (int i = 0; i < nt; ++i) pool.emplace_back(f, i, n * i / nt, n * (i + 1) / nt);
+  for (auto& t : pool) t.join();
+}
+
+
 int arg_error(const char* what) {
   std::snprintf(g_cerr, sizeof g_cerr, "%s", what);
   return MDI_E_ARG;
@@ -74,7 +93,8 @@ extern "C" {
 int64_t mdi_select(int64_t rows, const int64_t* tax_id, const int64_t* n_alignments, const int64_t* position,
                    const int64_t* counts16, const int32_t* strand_code, const uint8_t* code_is_fwd,
                    int32_t n_codes, const char* sub_fwd, const char* sub_rev, int64_t min_alignments,
-                   int64_t min_y_sum, int32_t* taxon, int64_t* y_sum_total, int64_t* perm) {
+                   int64_t min_y_sum, int n_threads, int32_t* taxon, int64_t* y_sum_total, int64_t* perm,
+                   int64_t* uniq, int64_t* n_taxa) {
   if (rows < 0 || (rows > 0 && (!tax_id || !n_alignments || !position || !counts16 || !strand_code ||
                                 !taxon || !y_sum_total || !perm)) ||
       n_codes < 0 || (n_codes > 0 && !code_is_fwd))
@@ -84,65 +104,130 @@ int64_t mdi_select(int64_t rows, const int64_t* tax_id, const int64_t* n_alignme
   const Rows R{rows, tax_id, n_alignments, position, counts16, strand_code, code_is_fwd, n_codes};
   const int64_t* yf = R.col(kf);
   const int64_t* yr = R.col(kr);
+  const int nt = pool_size(n_threads, rows);
 
-  // taxon index in first-appearance order (pd.factorize), looked up once per run of equal tax_id
-  std::unordered_map<int64_t, int32_t> index;
-  std::vector<int64_t> ysum;
-  int32_t cur = -1;
-  for (int64_t r = 0; r < rows; ++r) {
-    if (r == 0 || tax_id[r] != tax_id[r - 1]) {
-      auto it = index.emplace(tax_id[r], (int32_t)ysum.size());
-      if (it.second) ysum.push_back(0);
-      cur = it.first->second;
+  // (1) per row range: the runs of equal tax_id and their substitution sums
+  struct Run {
+    int64_t start, tax, ys;
+  };
+  std::vector<std::vector<Run>> runs((size_t)nt);
+  for_ranges(nt, rows, [&](int tid, int64_t lo, int64_t hi) {
+    std::vector<Run>& v = runs[(size_t)tid];
+    for (int64_t r = lo; r < hi; ++r) {
+      if (r == lo || tax_id[r] != tax_id[r - 1]) v.push_back({r, tax_id[r], 0});
+      const int64_t p = R.pos(r);
+      v.back().ys += p > 0 ? yf[r] : (p < 0 ? yr[r] : 0);
     }
-    taxon[r] = cur;
-    const int64_t p = R.pos(r);
-    ysum[cur] += p > 0 ? yf[r] : (p < 0 ? yr[r] : 0);
-  }
-  int64_t n_keep = 0;
-  for (int64_t r = 0; r < rows; ++r) {
-    y_sum_total[r] = ysum[taxon[r]];
-    if (n_alignments[r] >= min_alignments && y_sum_total[r] >= min_y_sum) perm[n_keep++] = r;
-  }
+  });
+  // (2) taxon index in first-appearance order (pd.factorize) over the runs, in file order
+  std::unordered_map<int64_t, int32_t> index;
+  std::vector<int64_t> ysum, utax;
+  std::vector<std::vector<int32_t>> run_id((size_t)nt);
+  for (int tid = 0; tid < nt; ++tid)
+    for (const Run& u : runs[(size_t)tid]) {
+      auto it = index.emplace(u.tax, (int32_t)ysum.size());
+      if (it.second) {
+        ysum.push_back(0);
+        utax.push_back(u.tax);
+      }
+      ysum[(size_t)it.first->second] += u.ys;
+      run_id[(size_t)tid].push_back(it.first->second);
+    }
+  // (3) per row: its taxon and y_sum_total, the cut; (4) the kept rows in file order
+  std::vector<int64_t> kept((size_t)nt + 1, 0);
+  for_ranges(nt, rows, [&](int tid, int64_t lo, int64_t hi) {
+    const std::vector<Run>& v = runs[(size_t)tid];
+    int64_t k = 0;
+    for (size_t j = 0; j < v.size(); ++j) {
+      const int32_t id = run_id[(size_t)tid][j];
+      const int64_t ys = ysum[(size_t)id];
+      const int64_t e = j + 1 < v.size() ? v[j + 1].start : hi;
+      for (int64_t r = v[j].start; r < e; ++r) {
+        taxon[r] = id;
+        y_sum_total[r] = ys;
+        k += n_alignments[r] >= min_alignments && ys >= min_y_sum;
+      }
+    }
+    kept[(size_t)tid + 1] = k;
+  });
+  for (int tid = 0; tid < nt; ++tid) kept[(size_t)tid + 1] += kept[(size_t)tid];
+  const int64_t n_keep = kept[(size_t)nt];
+  for_ranges(nt, rows, [&](int tid, int64_t lo, int64_t hi) {
+    int64_t w = kept[(size_t)tid];
+    for (int64_t r = lo; r < hi; ++r)
+      if (n_alignments[r] >= min_alignments && y_sum_total[r] >= min_y_sum) perm[w++] = r;
+  });
+  if (n_taxa) *n_taxa = (int64_t)utax.size();
+  if (uniq && !utax.empty()) std::memcpy(uniq, utax.data(), sizeof(int64_t) * utax.size());
 
   // sort_by_alignments.  Usual layout: every taxon's kept rows one contiguous
   // run, z order already descending within it, one N_alignments per run ->
   // sort the runs only.  Otherwise the full three-key sort (stable: ties keep
   // file order, as np.lexsort).
-  std::vector<int64_t> starts;
-  bool runs_ok = true;
-  {
-    std::vector<uint8_t> seen(ysum.size(), 0);
-    for (int64_t i = 0; i < n_keep && runs_ok; ++i) {
+  const int kt = pool_size(n_threads, n_keep);
+  std::vector<std::vector<int64_t>> tstarts((size_t)kt);
+  std::vector<uint8_t> tok((size_t)kt, 1);
+  for_ranges(kt, n_keep, [&](int tid, int64_t lo, int64_t hi) {
+    std::vector<int64_t>& st = tstarts[(size_t)tid];
+    for (int64_t i = lo; i < hi; ++i) {
       const int64_t r = perm[i];
       if (i == 0 || taxon[r] != taxon[perm[i - 1]]) {
-        if (seen[taxon[r]]) runs_ok = false;
-        seen[taxon[r]] = 1;
-        starts.push_back(i);
+        st.push_back(i);
       } else {
         const int64_t q = perm[i - 1];
-        if (!(order_key(R.pos(r)) < order_key(R.pos(q))) || n_alignments[r] != n_alignments[q]) runs_ok = false;
+        if (!(order_key(R.pos(r)) < order_key(R.pos(q))) || n_alignments[r] != n_alignments[q]) {
+          tok[(size_t)tid] = 0;
+          return;
+        }
       }
     }
+  });
+  bool runs_ok = true;
+  for (int tid = 0; tid < kt; ++tid) runs_ok = runs_ok && tok[(size_t)tid];
+  std::vector<int64_t> starts;
+  if (runs_ok) {
+    std::vector<uint8_t> seen(ysum.size(), 0);
+    for (int tid = 0; tid < kt && runs_ok; ++tid)
+      for (const int64_t i : tstarts[(size_t)tid]) {
+        const int32_t t = taxon[perm[i]];
+        if (seen[(size_t)t]) {
+          runs_ok = false;
+          break;
+        }
+        seen[(size_t)t] = 1;
+        starts.push_back(i);
+      }
   }
   if (runs_ok) {
     const size_t nb = starts.size();
-    std::vector<int64_t> bs(nb);
-    for (size_t b = 0; b < nb; ++b) bs[b] = (int64_t)b;
-    std::sort(bs.begin(), bs.end(), [&](int64_t a, int64_t b) {
-      const int64_t ra = perm[starts[a]], rb = perm[starts[b]];
-      if (n_alignments[ra] != n_alignments[rb]) return n_alignments[ra] > n_alignments[rb];
-      if (tax_id[ra] != tax_id[rb]) return tax_id[ra] > tax_id[rb];
-      return a < b;
-    });
-    std::vector<int64_t> out((size_t)n_keep);
-    int64_t w = 0;
-    for (size_t k = 0; k < nb; ++k) {
-      const int64_t b = bs[k];
-      const int64_t lo = starts[b], hi = (size_t)b + 1 < nb ? starts[b + 1] : n_keep;
-      for (int64_t i = lo; i < hi; ++i) out[w++] = perm[i];
+    struct Key {
+      int64_t nal, tax, b;
+    };
+    std::vector<Key> keys(nb);
+    for (size_t b = 0; b < nb; ++b) {
+      const int64_t r = perm[starts[b]];
+      keys[b] = {n_alignments[r], tax_id[r], (int64_t)b};
     }
-    std::memcpy(perm, out.data(), sizeof(int64_t) * (size_t)n_keep);
+    std::sort(keys.begin(), keys.end(), [](const Key& a, const Key& b) {
+      if (a.nal != b.nal) return a.nal > b.nal;
+      if (a.tax != b.tax) return a.tax > b.tax;
+      return a.b < b.b;
+    });
+    std::vector<int64_t> dst(nb + 1, 0);
+    for (size_t k = 0; k < nb; ++k) {
+      const int64_t b = keys[k].b;
+      const int64_t hi = (size_t)b + 1 < nb ? starts[(size_t)b + 1] : n_keep;
+      dst[k + 1] = dst[k] + (hi - starts[(size_t)b]);
+    }
+    std::vector<int64_t> out((size_t)n_keep);
+    for_ranges(pool_size(n_threads, (int64_t)nb * 32), (int64_t)nb, [&](int, int64_t lo, int64_t hi) {
+      for (int64_t k = lo; k < hi; ++k) {
+        const int64_t b = keys[(size_t)k].b;
+        std::memcpy(out.data() + dst[(size_t)k], perm + starts[(size_t)b],
+                    sizeof(int64_t) * (size_t)(dst[(size_t)k + 1] - dst[(size_t)k]));
+      }
+    });
+    if (n_keep > 0) std::memcpy(perm, out.data(), sizeof(int64_t) * (size_t)n_keep);
   } else {
     std::stable_sort(perm, perm + n_keep, [&](int64_t a, int64_t b) {
       if (n_alignments[a] != n_alignments[b]) return n_alignments[a] > n_alignments[b];
@@ -221,26 +306,6 @@ int mdi_gather(int64_t rows, const int64_t* perm, int64_t n_keep, const int64_t*
 const char* mdi_counts_error(void) { return g_cerr; }
 
 }  // extern "C"
-
-namespace {
-int pool_size(int n_threads, int64_t n) {
-  int nt = n_threads > 0 ? n_threads : mdi_default_threads();
-  if (nt < 1) nt = 1;
-  if (n < (int64_t)nt * 65536) nt = (int)std::max<int64_t>(1, n / 65536);
-  return nt > 64 ? 64 : nt;
-}
-
-template <typename F>
-void for_ranges(int nt, int64_t n, F f) {
-  if (nt <= 1) {
-    f(0, (int64_t)0, n);
-    return;
-  }
-  std::vector<std::thread> pool;
-  for (int i = 0; i < nt; ++i) pool.emplace_back(f, i, n * i / nt, n * (i + 1) / nt);
-  for (auto& t : pool) t.join();
-}
-}  // namespace
 
 extern "C" {
 

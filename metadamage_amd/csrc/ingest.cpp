@@ -440,7 +440,15 @@ int mdi_strings(const mdi_table* t, int which, char* buf, int64_t* offsets) {
 
 void mdi_free(mdi_table* t) {
   if (!t) return;
-  if (t->map && t->map != MAP_FAILED) munmap(t->map, t->size);
+  // unmapping a populated 300 MB mapping takes ~20 ms of page-table
+  // teardown: done on a detached thread (nothing views the mapping any more:
+  // the string tables were copied out by mdi_parse_into)
+  if (t->map && t->map != MAP_FAILED) {
+    void* m = t->map;
+    const size_t n = t->size;
+    if (n >= ((size_t)1 << 24)) std::thread([m, n] { munmap(m, n); }).detach();
+    else munmap(m, n);
+  }
   delete t;
 }
 

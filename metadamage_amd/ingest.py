@@ -52,7 +52,7 @@ def _load():
         lib.mdi_free.restype = None
         lib.mdi_last_error.restype = ctypes.c_char_p
         lib.mdi_select.argtypes = [i64, vp, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_char_p, ctypes.c_char_p,
-                                   i64, i64, vp, vp, vp]
+                                   i64, i64, ctypes.c_int, vp, vp, vp, vp, vp]
         lib.mdi_select.restype = i64
         lib.mdi_gather.argtypes = [i64, vp, i64, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_char_p,
                                    ctypes.c_char_p, vp, ctypes.c_int, vp, vp, vp, vp, vp, vp]
@@ -261,10 +261,14 @@ def compute_counts(cfg, table: Table | None = None, n_threads: int = 0) -> pd.Da
     perm = np.empty(n, np.int64)
     common = (t.position.ctypes.data, t.counts.ctypes.data, t.strand_code.ctypes.data, is_fwd.ctypes.data,
               len(is_fwd), fwd.encode(), rev.encode())
+    uniq = np.empty(n, np.int64)
+    n_taxa = ctypes.c_int64(0)
     k = lib.mdi_select(n, t.tax_id.ctypes.data, t.n_alignments.ctypes.data, *common, int(cfg.min_alignments),
-                       int(cfg.min_y_sum), taxon.ctypes.data, ysum.ctypes.data, perm.ctypes.data)
+                       int(cfg.min_y_sum), int(n_threads), taxon.ctypes.data, ysum.ctypes.data, perm.ctypes.data,
+                       uniq.ctypes.data, ctypes.byref(n_taxa))
     if k < 0:
         raise ValueError(lib.mdi_counts_error().decode())
+    uniq = uniq[:n_taxa.value]
     perm = perm[:k]
     nal = np.empty(k, np.uint32)
     pos = np.empty(k, np.int8)
@@ -277,7 +281,6 @@ def compute_counts(cfg, table: Table | None = None, n_threads: int = 0) -> pd.Da
                         f2.ctypes.data, ys.ctypes.data)
     if rc != 0:
         raise AssertionError(lib.mdi_counts_error().decode())
-    uniq = t.tax_id[np.flatnonzero(np.r_[True, taxon[1:] > np.maximum.accumulate(taxon[:-1])])] if n else t.tax_id
     if t.format == 22:
         cat_id, cat_name, cat_rank, cat_strand = _categoricals(
             perm, [(taxon, uniq), (t.name_code, t.names), (t.rank_code, t.ranks), (t.strand_code, t.strands)],

@@ -277,6 +277,51 @@ def test_native_pipeline_edge_layouts(tmp_path, layout):
     pd.testing.assert_frame_equal(ingest.compute_counts_numpy(cfg), want)
 
 
+@pytest.fixture(scope="module")
+def table_9000():
+    from metadamage_amd.synthetic import generate, to_counts_table
+
+    return to_counts_table(generate(9000, seed=34, fail_fraction=0.1))
+
+
+@pytest.mark.parametrize("layout", ["usual", "shuffled", "split_runs"])
+def test_native_pipeline_threads(tmp_path, layout, table_9000):
+    """mdi_select / mdi_gather over several row ranges (>= 65,536 rows per
+    thread): runs of a taxon cut by a range boundary, a taxon in two runs far
+    apart, and the full sort -- frame-identical to the numpy restatement and to
+    the one-thread call."""
+    from metadamage_amd import ingest
+
+    table = table_9000
+    if layout == "shuffled":
+        table = table.sample(frac=1, random_state=2)
+    elif layout == "split_runs":
+        n = len(table)
+        table = table.iloc[np.r_[np.arange(0, 45), np.arange(n // 2, n), np.arange(45, n // 2)]]
+    f = tmp_path / "t.tsv"
+    table.to_csv(f, sep="\t", header=False, index=False)
+    cfg = _cfg(f)
+    t = ingest.read_table(f, 3)
+    assert t.rows >= 4 * 65536
+    many = ingest.compute_counts(cfg, table=t, n_threads=4)
+    _assert_frames_identical(many, ingest.compute_counts(cfg, table=t, n_threads=1))
+    _assert_frames_identical(many, ingest.compute_counts_numpy(cfg, table=t))
+
+
+def _assert_frames_identical(a, b):
+    """assert_frame_equal for large frames: categoricals by categories + codes
+    (pandas boxes every value of a categorical column when comparing)."""
+    assert list(a.columns) == list(b.columns) and a.index.equals(b.index)
+    for c in a.columns:
+        x, y = a[c], b[c]
+        assert x.dtype == y.dtype, c
+        if isinstance(x.dtype, pd.CategoricalDtype):
+            assert x.cat.categories.equals(y.cat.categories), c
+            assert np.array_equal(x.cat.codes.to_numpy(), y.cat.codes.to_numpy()), c
+        else:
+            assert np.array_equal(x.to_numpy(), y.to_numpy(), equal_nan=x.dtype.kind == "f"), c
+
+
 def test_native_pipeline_uint32_overflow(tmp_path):
     """A kept count above uint32 raises as utils.py:338-339; in a row the cut
     drops it does not."""
