@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 from dataclasses import dataclass
 from pathlib import Path
 
@@ -131,18 +132,38 @@ class Table:
         return len(self.tax_id)
 
 
-def read_table(path, n_threads: int = 0) -> Table:
-    """Parse a count table with the native reader."""
+_SCRATCH = threading.local()
+
+
+def _scratch(name: str, shape, dtype) -> np.ndarray:
+    """A per-thread array reused across calls: compute_counts' intermediates
+    (the parsed columns, the cut's index arrays; ~0.5 GB per 100k-taxon file)
+    are dropped once the output columns are gathered, and refilling mapped
+    pages spares the kernel's zeroing of fresh ones -- the pipeline's reader
+    threads are bound by host memory traffic."""
+    d = _SCRATCH.__dict__.setdefault("arrays", {})
+    n = int(np.prod(shape))
+    a = d.get(name)
+    if a is None or a.size < n or a.dtype != np.dtype(dtype):
+        a = d[name] = np.empty(n + n // 8, dtype)
+    return a[:n].reshape(shape)
+
+
+def read_table(path, n_threads: int = 0, scratch: bool = False) -> Table:
+    """Parse a count table with the native reader.  scratch: the numeric
+    columns live in this thread's reused buffers (valid until its next
+    scratch call; compute_counts)."""
     lib = _load()
     h = ctypes.c_void_p()
     rc = lib.mdi_open(os.fsencode(str(path)), int(n_threads), ctypes.byref(h))
     if rc != 0:
         raise FileNotFoundError(f"{path}: {lib.mdi_last_error().decode()}")
+    alloc = _scratch if scratch else (lambda name, shape, dtype: np.empty(shape, dtype))
     try:
         n = int(lib.mdi_rows(h))
-        cols = [np.empty(n, np.int64) for _ in range(3)]
-        counts = np.empty((16, n), np.int64)  # column-major: one contiguous array per base pair
-        codes = [np.empty(n, np.int32) for _ in range(3)]
+        cols = [alloc(f"col{i}", n, np.int64) for i in range(3)]
+        counts = alloc("counts", (16, n), np.int64)  # column-major: one contiguous array per base pair
+        codes = [alloc(f"code{i}", n, np.int32) for i in range(3)]
         # (no pre-fault: the parser threads first-touch their own row ranges in
         # parallel -- faulting ~470 MB here on one thread cost more than the parse)
         rc = lib.mdi_parse_into(h, *(c.ctypes.data for c in cols), counts.ctypes.data,
@@ -252,23 +273,23 @@ def compute_counts(cfg, table: Table | None = None, n_threads: int = 0) -> pd.Da
     csrc/counts.cpp); the categoricals from the interned string codes.  Same
     frame as compute_counts_numpy and counts.compute_counts_pandas."""
     lib = _load()
-    t = read_table(cfg.filename, n_threads) if table is None else table
+    t = read_table(cfg.filename, n_threads, scratch=True) if table is None else table
     fwd, rev = cfg.substitution_bases_forward, cfg.substitution_bases_reverse
     n = t.rows
     is_fwd = np.ascontiguousarray(t.strands == "5'", dtype=np.uint8)
-    taxon = np.empty(n, np.int32)
-    ysum = np.empty(n, np.int64)
-    perm = np.empty(n, np.int64)
+    taxon = _scratch("taxon", n, np.int32)
+    ysum = _scratch("ysum", n, np.int64)
+    perm = _scratch("perm", n, np.int64)
     common = (t.position.ctypes.data, t.counts.ctypes.data, t.strand_code.ctypes.data, is_fwd.ctypes.data,
               len(is_fwd), fwd.encode(), rev.encode())
-    uniq = np.empty(n, np.int64)
+    uniq = _scratch("uniq", n, np.int64)
     n_taxa = ctypes.c_int64(0)
     k = lib.mdi_select(n, t.tax_id.ctypes.data, t.n_alignments.ctypes.data, *common, int(cfg.min_alignments),
                        int(cfg.min_y_sum), int(n_threads), taxon.ctypes.data, ysum.ctypes.data, perm.ctypes.data,
                        uniq.ctypes.data, ctypes.byref(n_taxa))
     if k < 0:
         raise ValueError(lib.mdi_counts_error().decode())
-    uniq = uniq[:n_taxa.value]
+    uniq = uniq[:n_taxa.value].copy()
     perm = perm[:k]
     nal = np.empty(k, np.uint32)
     pos = np.empty(k, np.int8)
