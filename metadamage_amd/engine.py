@@ -195,7 +195,7 @@ def staging(capacity: int, device="cuda", opts: _lib.MdfitOpts | None = None, wi
     process (per device and buffer set): the multi-file pipeline fits one file
     after another, and pinned + device buffers of ~2.3 KB (+ the ~4.8 KB MAP
     workspace) per taxon allocated per file cost more host time than the fit.
-    Grown (x1.25 headroom) when a larger batch comes; fit_batch_host holds
+    Sized with x1.25 headroom, grown when a larger batch comes; fit_batch_host holds
     _STAGING_LOCK around its use (concurrent host threads take turns)."""
     torch = _torch()
     dev = torch.device(device)
@@ -206,7 +206,10 @@ def staging(capacity: int, device="cuda", opts: _lib.MdfitOpts | None = None, wi
     st = _STAGING.get(key)
     if st is None or st.capacity < capacity:
         _STAGING.pop(key, None)
-        st = HostStaging(max(int(capacity), int(1.25 * st.capacity) if st is not None else 0), device=dev, opts=o,
+        # x1.25 headroom from the first allocation on: the files of a run
+        # differ in taxon count by a few %, and a regrow (pinned + device
+        # buffers, ~0.15 s at 100k taxa) costs more than the spare memory
+        st = HostStaging(int(1.25 * max(int(capacity), st.capacity if st is not None else 0)), device=dev, opts=o,
                          with_mm=with_mm)
         _STAGING[key] = st
     return st
