@@ -137,7 +137,8 @@ void mdfit_default_opts(mdfit_opts* opts);
  *   status    : int32_t[n_taxa]                             (device)
  *   workspace : device buffer of mdfit_workspace_bytes(n_taxa) bytes (work
  *               queues, the PMD-all mode for the HPDI, the wide-window list:
- *               MAP 256 B + 4,832 B per taxon)
+ *               MAP 256 B + 48 B per taxon below 60k taxa, + 4,800 B more
+ *               per taxon from 60k)
  *   hip_stream: hipStream_t or NULL.  MAP: the record assembly runs on a
  *               library-owned side stream (one per device, created once),
  *               forked from and joined back into hip_stream by events on every

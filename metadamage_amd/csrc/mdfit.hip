@@ -1202,7 +1202,11 @@ using mdfit::host::set_err;
 // per call, events around the whole call and around fit_kernel, on the
 // caller's stream
 constexpr int kProfMax = 256;
-constexpr int64_t kPpl2MinTaxa = 35000;  // measured crossover: 30-40k taxa (PPL 1 fuses the HPDI prep)
+// measured crossovers (profiles/r03_layout_crossovers.jsonl):
+// the 2-points-per-lane layout from 12.5-15k taxa (with the HPDI streamed
+// beside the fit), the HPDI after the fit from 50-65k
+constexpr int64_t kPpl2MinTaxa = 13000;
+constexpr int64_t kStreamMaxTaxa = 60000;
 struct ProfState {
   bool on = false;
   bool fit_only = false;  // mdfit_profile_enable(2): only the events around fit_kernel
@@ -1232,7 +1236,7 @@ double* ready_buf(void* ws) { return reinterpret_cast<double*>(static_cast<char*
 mdfit::hpdi::WideRec* hpdi_recs(void* ws) {
   return reinterpret_cast<mdfit::hpdi::WideRec*>(static_cast<char*>(ws) + 256);
 }
-// (the fit's K4a / K4b path from kPpl2MinTaxa taxa: after the ready list)
+// (the fit's K4a / K4b path from kStreamMaxTaxa taxa: after the ready list)
 mdfit::hpdi::WideRec* hpdi_recs_after_ready(void* ws, int64_t n_taxa) {
   return reinterpret_cast<mdfit::hpdi::WideRec*>(static_cast<char*>(ws) + 256 +
                                                  n_taxa * mdfit::kReadyStride * (int64_t)sizeof(double));
@@ -1373,10 +1377,10 @@ int64_t mdfit_workspace_bytes(int64_t n_taxa, const mdfit_opts* opts) {
   if (opts) o = *opts;
   if (o.mode == MDFIT_MODE_NUTS) return mdfit::nuts::workspace_bytes(n_taxa, o.num_samples);
   // the 256-byte header (counters, flags), then the ready list of
-  // PMD-all modes (48 B per taxon); from kPpl2MinTaxa taxa (the HPDI after the
-  // fit, K4a -> K4b) room for every position's wide-window record
+  // PMD-all modes (48 B per taxon); from kStreamMaxTaxa taxa (the HPDI after
+  // the fit, K4a -> K4b) room for every position's wide-window record
   return 256 + n_taxa * mdfit::kReadyStride * (int64_t)sizeof(double) +
-         (n_taxa >= kPpl2MinTaxa ? n_taxa * mdfit::kNPos * (int64_t)sizeof(mdfit::hpdi::WideRec) : 0);
+         (n_taxa >= kStreamMaxTaxa ? n_taxa * mdfit::kNPos * (int64_t)sizeof(mdfit::hpdi::WideRec) : 0);
 }
 
 int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t n_taxa,
@@ -1424,12 +1428,12 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   // K4 (early): the predictive HPDI streamed beside the fit kernel, on side
   // stream 0 from after K0; its grid -- MDFIT_STREAM_WAVES_PER_CU waves per CU
   // -- is the room the fit kernel's grid leaves
-  // The HPDI streams beside the fit below kPpl2MinTaxa taxa -- the regime where
+  // The HPDI streams beside the fit below kStreamMaxTaxa taxa -- the regime where
   // the call is bounded by the fit kernel's tail, which the stream fills --
   // and runs after the fit from there (the fit kernel fills the chip by itself;
   // K4a -> K4b at full occupancy, longest windows first).  MDFIT_HPDI_STREAM=1
   // streams at any size (A/B; the workspace has no wide-window list below).
-  bool stream = n_taxa < kPpl2MinTaxa;
+  bool stream = n_taxa < kStreamMaxTaxa;
   if (const char* e = std::getenv("MDFIT_HPDI_STREAM")) stream = stream || std::atoi(e) != 0;
   const int early_per_cu =
       (fk != nullptr && stream) ? env_int("MDFIT_STREAM_WAVES_PER_CU", MDFIT_STREAM_WAVES_PER_CU) : 0;

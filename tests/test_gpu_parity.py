@@ -295,11 +295,11 @@ def test_bench_size_properties(engine, oracle_lib):
 
 
 def test_lane_layouts_are_bitwise_identical(engine, monkeypatch):
-    """The fit kernel's two lane layouts (1 point per lane below 35k taxa, 2
+    """The fit kernel's two lane layouts (1 point per lane below 13k taxa, 2
     above) sum in the same tree order, so a taxon's record does
     not depend on the batch size that picked the layout -- nor on where the
-    predictive HPDI's per-position step ran (fused into the PPL-1 fit kernel, or
-    hpdi_prep_kernel after PPL 2)."""
+    predictive HPDI ran (streamed beside the fit kernel below 60k taxa, K4a /
+    K4b after it above)."""
     from metadamage_amd.synthetic import generate
 
     b = generate(3_000, seed=11)
@@ -309,10 +309,13 @@ def test_lane_layouts_are_bitwise_identical(engine, monkeypatch):
         res[ppl] = engine.fit_batch(b.y, b.N, b.mm)
     for a, c in zip(res["1"], res["2"]):
         assert np.array_equal(a, c, equal_nan=True)
-    # and a taxon fitted inside a batch above the threshold matches it too
+    # and a taxon fitted inside larger batches matches it too: 16k (2 points
+    # per lane, HPDI streamed) and 66k (HPDI after the fit)
     monkeypatch.delenv("MDFIT_FIT_PPL")
-    more = generate(33_000, seed=12)  # 36k in all: above the 35k switch
-    cat = [np.concatenate([getattr(b, f), getattr(more, f)]) for f in ("y", "N", "mm")]
-    out_big, pred_big, st_big = engine.fit_batch(*cat)
-    assert np.array_equal(out_big[:3_000], res["1"][0], equal_nan=True)
-    assert np.array_equal(pred_big[:3_000], res["1"][1], equal_nan=True)
+    more = generate(63_000, seed=12)
+    for extra in (13_000, 63_000):
+        cat = [np.concatenate([getattr(b, f), getattr(more, f)[:extra]]) for f in ("y", "N", "mm")]
+        out_big, pred_big, st_big = engine.fit_batch(*cat)
+        assert np.array_equal(out_big[:3_000], res["1"][0], equal_nan=True)
+        assert np.array_equal(pred_big[:3_000], res["1"][1], equal_nan=True)
+        assert np.array_equal(st_big[:3_000], res["1"][2])

@@ -27,6 +27,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--taxa", type=int, default=10_000)
     ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--configs", default="", help='JSON list of [name, {env}] (default: the stream-grid sweep)')
     a = ap.parse_args()
     import torch
 
@@ -44,6 +45,8 @@ def main() -> None:
                ("early4_fit6", {"MDFIT_STREAM_WAVES_PER_CU": "4", "MDFIT_FIT_WAVES_PER_CU": "6"}),
                ("early4_prio0", {"MDFIT_FIT_BASE_PRIO": "0"}),
                ("default_again", {})]
+    if a.configs:
+        configs = [tuple(c) for c in json.loads(a.configs)]
     keys = {k for _, e in configs for k in e}
     ref = None
     for name, env in configs:
