@@ -65,6 +65,10 @@ def main() -> None:
         pass
     write_summary(prof, tag, "fit_kernel", TAXA, FIT_BYTES_PER_TAXON, 448, found["kernel_stats.csv"],
                   found["pmc_fetch_size.csv"], found["pmc_write_size.csv"], "python bench.py", handoff)
+    sq = sorted((src / "sq").rglob("*counter_collection.csv"))
+    if sq:
+        shutil.copy(sq[0], prof / f"{tag}_pmc_sq.csv")
+        sq_decomposition(prof, tag, prof / f"{tag}_pmc_sq.csv")
     # the NUTS chain kernel at config C3 (optional passes)
     nf, nw = sorted((src / "nuts_fetch").rglob("*counter_collection.csv")), sorted((src / "nuts_write").rglob("*counter_collection.csv"))
     if nuts and nf and nw:
@@ -73,6 +77,33 @@ def main() -> None:
         write_summary(prof, tag, "nuts_chain_kernel", NUTS_TAXA, NUTS_BYTES_PER_TAXON, 808,
                       prof / f"{tag}_nuts_kernel_stats.csv", prof / f"{tag}_nuts_pmc_fetch_size.csv",
                       prof / f"{tag}_nuts_pmc_write_size.csv", "python bench.py --mode nuts")
+
+
+def sq_decomposition(prof, tag, sq_csv):
+    """Per kernel: the SQ counters as fractions of SQ_WAVE_CYCLES (summed over
+    dispatches), instructions per wave, SALU per VALU."""
+    acc = {}
+    for r in rows(sq_csv):
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        if "mdfit" not in k:
+            continue
+        d = acc.setdefault(k, {"dispatches": set()})
+        d["dispatches"].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    out = {}
+    for k, d in acc.items():
+        cyc = d.get("SQ_WAVE_CYCLES", 0.0)
+        if cyc <= 0:
+            continue
+        out[k] = {"dispatches": len(d["dispatches"]),
+                  **{n.replace("SQ_", "").lower(): round(d.get(n, 0.0) / cyc, 3) for n in
+                     ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU")},
+                  "valu_insts_per_wave": round(d.get("SQ_INSTS_VALU", 0.0) / max(d.get("SQ_WAVES", 1.0), 1.0), 1),
+                  "salu_per_valu": round(d.get("SQ_INSTS_SALU", 0.0) / max(d.get("SQ_INSTS_VALU", 1.0), 1.0), 3)}
+    note = ("fractions of SQ_WAVE_CYCLES (MI355X_MICROARCH.md: WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~ "
+            "WAVE_CYCLES); one rocprofv3 --pmc pass of 8 SQ counters over python bench.py (C2, MAP)")
+    (prof / f"{tag}_sq_decomposition.json").write_text(json.dumps({"C2 MAP": out, "note": note}, indent=1) + "\n")
+    print(json.dumps(out, indent=1))
 
 
 def write_summary(prof, tag, name, taxa, bytes_per_taxon, alg_per_taxon, stats_csv, fetch_csv, write_csv, cmd,
