@@ -55,8 +55,8 @@ def main() -> None:
     for name in ("bench_trace.json", "bench_nuts_trace.json"):
         if (src / name).exists():
             shutil.copy(src / name, prof / f"{tag}_{name}")
-    # the fit kernel's hand-off as the traced bench run reports it (the record,
-    # plus at PPL 1 the fused HPDI step's wide-window list and greedy bounds)
+    # the fit kernel's hand-off as the traced bench run reports it (the record
+    # and the ready-list entries)
     handoff = None
     try:
         line = next(json.loads(x) for x in open(src / "bench_trace.json") if x.startswith("{"))
@@ -122,8 +122,8 @@ def write_summary(prof, tag, name, taxa, bytes_per_taxon, alg_per_taxon, stats_c
         "reads; this kernel's 4-B/lane and broadcast 8-B loads are uncalibrated), WRITE_SIZE x1",
         "hbm_bytes_per_launch": int(round((2 * fetch_kb + write_kb) * 1024)),
         "handoff_bytes_per_launch": handoff_override if handoff_override else bytes_per_taxon * taxa,
-        "handoff_note": "what the kernel moves as built (the hand-off to the next kernels: MAP the 6 sub-fit records "
-        "and, PPL 1, the fused HPDI step's wide-window list and greedy bounds; NUTS the draws)",
+        "handoff_note": "what the kernel moves as built (the hand-off to the next kernels: MAP y,N + the 6 initial "
+        "points in, the 6 sub-fit records and the 48-B ready-list entry per taxon out; NUTS the draws)",
         "survey_algorithmic_bytes_per_launch": alg_per_taxon * taxa,
         "survey_note": "SURVEY.md 8(d): y,N in + 26 result fields out (+ 90 prediction values for NUTS)",
         "rocprof_avg_ns": float(fk.get("AverageNs", "nan")),
