@@ -65,14 +65,17 @@ def main() -> None:
             full = res.out.cpu().numpy()
             out = full[:, :25]
             st = res.status.cpu().numpy()
+            pred = res.pred.cpu().numpy()
             if ref is None:
-                ref = out
+                ref, ref_pred = out, pred
+            same_pred = np.array_equal(pred, ref_pred, equal_nan=True)
             rel = np.abs(out - ref) / (np.abs(ref) + 1e-300)
             dev = np.nanmax(rel)
             ndiff = int((np.nan_to_num(rel, nan=0.0).max(1) > 1e-9).sum())
             evals = full[:, _lib.F_DIAG + 5::8][:, :6].sum() if a.mode == "map" else float("nan")
             print(f"rep {rep} {Path(path).name:24s} {ms:8.3f} ms  {a.taxa / ms * 1e3 / 1e6:6.2f} M fits/s  "
-                  f"ok {np.mean(st == 0):.4f}  max rel dev vs first {dev:.1e} ({ndiff} taxa)  evals {evals:.0f}",
+                  f"ok {np.mean(st == 0):.4f}  max rel dev vs first {dev:.1e} ({ndiff} taxa)  pred identical {same_pred}  "
+                  f"evals {evals:.0f}",
                   flush=True)
 
 
