@@ -143,7 +143,12 @@ void mdfit_default_opts(mdfit_opts* opts);
  *               library-owned side stream (one per device, created once),
  *               forked from and joined back into hip_stream by events on every
  *               return path, so the call stays ordered on hip_stream and
- *               capturable in a graph
+ *               capturable in a graph.  MAP below 60k taxa: the predictive
+ *               HPDI kernel runs beside the fit kernel and waits for modes
+ *               the fit kernel's waves publish; the two grids are sized to be
+ *               co-resident on an otherwise idle device.  Run calls on one
+ *               device one after another (one stream, or ordered streams),
+ *               not concurrently with other long-running kernels.
  *   n_taxa    : at most 2^25 per call (MAP: int32 position indices)
  * Replaces compute_fits' per-taxon loop (fits.py:477-526, 569-626, 709-730).
  */

@@ -954,18 +954,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
 // per CU; the fit kernel's grid leaves them room), so the HPDI work fills the
 // fit kernel's idle issue slots and its tail; and one after fit_kernel on the
 // caller's stream, full occupancy, for what is left.
-// Waiting, deadlock-free by construction: a kEarly wave claims only items of
-// entries already allocated in the ready list (bounded claims, one CAS per
-// wave-trip), whose writer -- a fit wave past its atomicAdd, resident and
-// running -- stores the tag within a few instructions; it never holds a claim
-// on an entry whose fit may not be running (the fit kernel's per-XCD queues
-// are served only by their own waves, and a queue whose waves could not get a
-// slot next to this kernel's would otherwise never publish).  With nothing
-// claimable it sleeps, and leaves once no entry has appeared for kStallTicks
-// (or the fit kernel has not started within ~50 us): what it leaves is the
-// late launch's, which runs after the fit and never waits.  Every wave exits
-// once the claim counter reaches T * per.
-constexpr uint64_t kStallTicks = 20000;  // 200 us at s_memrealtime's 100 MHz
+// Waiting: a kEarly wave waits on entries only after it has seen fit_kernel's
+// started flag -- a started fit kernel completes whatever this kernel does,
+// and publishes all T entries -- and exits when the flag has not appeared
+// within ~50 us (its launch may have been queued behind this one: the two
+// streams can share a hardware queue); the late launch never waits.  Every
+// wave exits once the claim counter passes T * per.
 #ifndef MDFIT_STREAM_WAVES_PER_CU
 #define MDFIT_STREAM_WAVES_PER_CU 4  // A/B at 10k and 125k taxa (tools/overlap_exp.py): 4 with the fit waves' base priority 1
 #endif
@@ -993,58 +987,17 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
   hpdi::Wide& W = sW[lane];
   int64_t item = 0, oitem = 0;  // the claimed item; its output index taxon * per + position
   bool busy = false, pending = false, drained = false;
-  // kEarly: the ready-list length last seen and when it last grew
-  int seen_ready = 0;
-  uint64_t t_grew = __builtin_amdgcn_s_memrealtime();
   while (true) {
     const bool need = !busy && !pending && !drained;
     const unsigned long long m = __ballot(need);
     if (m != 0ull) {
-      int base = 0, got = 0;  // got < 0: the counter has reached n_items
-      int rdy = 0;
-      if (lane == 0) {
-        const int want = __popcll(m);
-        if (kEarly) {
-          int c = __hip_atomic_load(ws + kWsClaim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          while (true) {
-            if ((int64_t)c >= n_items) {
-              got = -1;
-              break;
-            }
-            rdy = __hip_atomic_load(ws + kWsReady, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int64_t room = min((int64_t)rdy * per, n_items) - c;
-            const int k = room < (int64_t)want ? (int)max(room, (int64_t)0) : want;
-            if (k == 0) break;
-            if (__hip_atomic_compare_exchange_strong(ws + kWsClaim, &c, c + k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT)) {
-              base = c;
-              got = k;
-              break;
-            }
-          }
-        } else {
-          base = atomicAdd(ws + kWsClaim, want);
-          got = want;
-        }
-      }
-      if (kEarly) {
-        // wave-uniform: the ready-list length and when it last grew; nothing
-        // new for kStallTicks -> leave the rest to the late launch
-        const int r0 = __builtin_amdgcn_readfirstlane(rdy);
-        const uint64_t now = __builtin_amdgcn_s_memrealtime();
-        if (r0 != seen_ready) {
-          seen_ready = r0;
-          t_grew = now;
-        }
-        if (__builtin_amdgcn_readfirstlane(got) == 0 && now - t_grew > kStallTicks && lane == 0) got = -1;
-      }
+      int base = 0;
+      if (lane == 0) base = atomicAdd(ws + kWsClaim, __popcll(m));
       base = __shfl(base, 0);
-      got = __shfl(got, 0);
       if (need) {
-        const int rk = __popcll(m & ((1ull << lane) - 1ull));
-        const int64_t it = (int64_t)base + rk;
-        if (got < 0 || (!kEarly && it >= n_items)) drained = true;
-        else if (rk < got) {
+        const int64_t it = (int64_t)base + __popcll(m & ((1ull << lane) - 1ull));
+        if (it >= n_items) drained = true;
+        else {
           item = it;
           pending = true;
         }
@@ -1095,7 +1048,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
         busy = false;
       }
     }
-    if (!__any(prog)) __builtin_amdgcn_s_sleep(8);  // every lane waits for an entry or a claimable item
+    if (!__any(prog)) __builtin_amdgcn_s_sleep(8);  // every lane waits on an entry still being fitted
   }
 }
 
@@ -1313,13 +1266,8 @@ Fork* side_fork() {
   std::lock_guard<std::mutex> g(make_mu);
   if (!x.ok) {
     bool ok = true;
-    // MDFIT_SIDE0_PRIO (development A/B): side stream 0 (the HPDI stream
-    // kernel's) created with that HIP stream priority
-    const char* pe = std::getenv("MDFIT_SIDE0_PRIO");
     for (int k = 0; k < 2 && ok; ++k)
-      ok = (x.s[k] != nullptr ||
-            (k == 0 && pe ? hipStreamCreateWithPriority(&x.s[k], hipStreamNonBlocking, std::atoi(pe))
-                          : hipStreamCreateWithFlags(&x.s[k], hipStreamNonBlocking)) == hipSuccess) &&
+      ok = (x.s[k] != nullptr || hipStreamCreateWithFlags(&x.s[k], hipStreamNonBlocking) == hipSuccess) &&
            (x.fork[k] != nullptr || hipEventCreateWithFlags(&x.fork[k], hipEventDisableTiming) == hipSuccess) &&
            (x.join[k] != nullptr || hipEventCreateWithFlags(&x.join[k], hipEventDisableTiming) == hipSuccess);
     if (!ok) return nullptr;  // (what was created is kept for the next try)
@@ -1490,18 +1438,12 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   const int early_per_cu =
       (fk != nullptr && stream) ? env_int("MDFIT_STREAM_WAVES_PER_CU", MDFIT_STREAM_WAVES_PER_CU) : 0;
   ForkScope fork_hp(early_per_cu > 0 ? fk : nullptr, s, 0);
-  // MDFIT_STREAM_AFTER (development A/B): the early launch enqueued after the
-  // fit kernel's, which then takes its full occupancy (the stream's waves get
-  // the slots the fit waves free)
-  const bool after = env_int("MDFIT_STREAM_AFTER", 0) != 0;
-  auto launch_early = [&]() -> int {
+  if (early_per_cu > 0) {
     const int64_t g = fit_grid(mdfit::hpdi_stream_kernel<true>, n_items, mdfit::kWave, early_per_cu);
     hipLaunchKernelGGL(mdfit::hpdi_stream_kernel<true>, dim3((unsigned)g), dim3(mdfit::kWave), 0, fork_hp.side(), N,
                        n_taxa, per, out, pred, ws, (const double*)ready);
-    return check_launch("hpdi_stream_kernel");
-  };
-  if (early_per_cu > 0 && !after)
-    if (int rc = launch_early()) return rc;
+    if (int rc = check_launch("hpdi_stream_kernel")) return rc;
+  }
   prof_record(1, s);
   {
     // fit waves above the HPDI stream's (whose waves then take the issue slots
@@ -1511,21 +1453,19 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
     const int cap_env = env_int("MDFIT_FIT_WAVES_PER_CU", 0);
     if (ppl == 2) {
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, mdfit::fit_kernel<2>, mdfit::kWave, 0) != hipSuccess) occ = 8;
-      const int cap = cap_env > 0 ? cap_env : std::max(1, occ - (after ? 0 : early_per_cu));
+      const int cap = cap_env > 0 ? cap_env : std::max(1, occ - early_per_cu);
       const int64_t g = fit_grid(mdfit::fit_kernel<2>, 2 * n_taxa, 4, cap);
       hipLaunchKernelGGL(mdfit::fit_kernel<2>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, y, N, n_taxa,
                          o.max_iter, o.tol_step, out, ws, ready, fit_prio);
     } else {
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, mdfit::fit_kernel<1>, mdfit::kWave, 0) != hipSuccess) occ = 8;
-      const int cap = cap_env > 0 ? cap_env : std::max(1, occ - (after ? 0 : early_per_cu));
+      const int cap = cap_env > 0 ? cap_env : std::max(1, occ - early_per_cu);
       const int64_t g = fit_grid(mdfit::fit_kernel<1>, 2 * n_taxa, 2, cap);
       hipLaunchKernelGGL(mdfit::fit_kernel<1>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, y, N, n_taxa,
                          o.max_iter, o.tol_step, out, ws, ready, fit_prio);
     }
   }
   if (int rc = check_launch("fit_kernel")) return rc;
-  if (early_per_cu > 0 && after)
-    if (int rc = launch_early()) return rc;
   prof_record(2, s);
   // then a fork: the record assembly (K3) on side stream 1, the HPDI's late
   // launch on the caller's stream (full occupancy, draining what the early
