@@ -102,7 +102,7 @@ def gather_records(buf, n_cap: int, rank: int, world: int, group=None, async_op:
     precede any reuse of `buf` or any read of `parts`)."""
     import torch.distributed as dist
 
-    if world == 1:
+    if world == 1 and not (dist.is_available() and dist.is_initialized()):
         return ([buf], None) if async_op else [buf]
     if buf.is_cuda and dist.get_backend(group) == "gloo":
         buf = buf.cpu()
@@ -112,13 +112,14 @@ def gather_records(buf, n_cap: int, rank: int, world: int, group=None, async_op:
 
 
 def all_ranks_agree(flag: bool) -> bool:
-    """True iff `flag` is true on every rank (a one-int all-reduce; world 1: flag).
+    """True iff `flag` is true on every rank (a one-int all-reduce; no process
+    group: flag).
     Used so that all ranks take the same branch before a collective (e.g. a
     cache hit must skip the fit on every rank or on none)."""
     import torch
     import torch.distributed as dist
 
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return bool(flag)
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
     t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)

@@ -174,15 +174,19 @@ def fit_packed(p: Packed, opts=None, shard: bool = True):
         raise _lib.MdfitError("metadamage_amd fits run on MI355X GPUs only (no HIP device visible)")
     import torch.distributed as dist
 
-    world = dist.get_world_size() if shard and dist.is_available() and dist.is_initialized() else 1
-    rank = dist.get_rank() if world > 1 else 0
+    # the sharded branch whenever a process group is up (a world of one
+    # included: one gather to itself, which is how a one-GPU box runs the
+    # RCCL path, tests/test_gpu_distributed.py)
+    grouped = shard and dist.is_available() and dist.is_initialized()
+    world = dist.get_world_size() if grouped else 1
+    rank = dist.get_rank() if grouped else 0
     dev = torch.device("cuda", torch.cuda.current_device())
     # add_noise_estimates (fits.py:359-376) runs in the assembly kernel on the
     # shipped mismatch counts: 1,440 B/taxon of asynchronous PCIe (~0.7 ms per
     # 10k taxa, bench host_to_host) costs no host time, while the host
     # statistics (ingest.noise) take ~1.5 ms of CPU per 10k taxa on the 16-thread
     # share of a multi-file pipeline that is host-bound
-    if world == 1:
+    if not grouped:
         return engine.fit_batch_host(p.y, p.N, p.mm, opts)
     lo, hi = shard_range(p.n_taxa, rank, world)
     if opts is not None:  # the sampler's streams are keyed by the global taxon index

@@ -78,3 +78,59 @@ def test_sharded_fit_packed_equals_single_process(mode_name):
     assert np.array_equal(st, ref_st)
     assert np.array_equal(out[:, :_lib.NRESULT], ref_out[:, :_lib.NRESULT], equal_nan=True)
     assert np.array_equal(pred, ref_pred, equal_nan=True)
+
+
+def _rccl_rank(port, T, q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    try:
+        # as distributed.init_from_env joins a torchrun job: the rank's GPU
+        # first, then the RCCL group bound to it
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        from metadamage_amd import distributed, fits
+        from metadamage_amd.synthetic import generate
+
+        assert dist.get_backend() == "nccl"
+        agree = (distributed.all_ranks_agree(True), distributed.all_ranks_agree(False))
+        b = generate(T, seed=29)
+        p = fits.Packed(b.tax_id, b.tax_id.astype(str), np.full(T, "species"), b.N_alignments, b.y, b.N, b.mm)
+        res = fits.fit_packed(p, None, shard=True)  # the sharded branch: device records, one RCCL gather
+        q.put((agree, [np.asarray(a) for a in res]))
+        distributed.shutdown(ok=True)
+    except Exception as e:  # surfaced by the parent
+        q.put(repr(e))
+
+
+def test_rccl_path_in_a_world_of_one():
+    """The RCCL ("nccl") branches of the multi-GPU path on the one GPU of the
+    box: the group joined as init_from_env does, the agreement all-reduce on
+    a device int, fit_packed's sharded branch with its device-buffer gather
+    to rank 0 and the batched D2H of unpack_gathered, shutdown's barrier --
+    bit-identical to the unsharded fit."""
+    import torch
+    import torch.multiprocessing as mp
+
+    from metadamage_amd import fits
+    from metadamage_amd.synthetic import generate
+
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test selected but no HIP device is visible")
+    T = 777
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pr = ctx.Process(target=_rccl_rank, args=(_free_port(), T, q))
+    pr.start()
+    got = q.get(timeout=300)
+    pr.join(timeout=120)
+    assert not isinstance(got, str), got
+    agree, (out, pred, st) = got
+    assert agree == (True, False)
+    b = generate(T, seed=29)
+    p = fits.Packed(b.tax_id, b.tax_id.astype(str), np.full(T, "species"), b.N_alignments, b.y, b.N, b.mm)
+    ref_out, ref_pred, ref_st = fits.fit_packed(p, None, shard=False)
+    assert np.array_equal(st, ref_st)
+    assert np.array_equal(out[:, :25], ref_out[:, :25], equal_nan=True)
+    assert np.array_equal(pred, ref_pred, equal_nan=True)
