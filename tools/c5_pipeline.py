@@ -135,6 +135,7 @@ def main() -> None:
     ap.add_argument("--stages", type=int, default=2, help="files to time stage by stage first (0: none)")
     ap.add_argument("--gen-procs", type=int, default=8)
     ap.add_argument("--readers", type=int, default=0, help="files read ahead (main.N_READERS; 0: its default)")
+    ap.add_argument("--arrow-threads", type=int, default=0, help="pyarrow.set_cpu_count (0: Arrow's default)")
     ap.add_argument("--trace", action="store_true", help="print the per-thread stage timeline of the driver run")
     a = ap.parse_args()
     import torch
@@ -170,6 +171,10 @@ def main() -> None:
     cfg.add_filenames(files)
     if a.readers:
         driver.N_READERS = a.readers
+    if a.arrow_threads:
+        import pyarrow
+
+        pyarrow.set_cpu_count(a.arrow_threads)
     if world > 1:
         dist.barrier()
     events = _trace_wrappers() if a.trace else None
