@@ -181,8 +181,11 @@ constexpr int kPrioEvals = 15;  // fit length (evaluations) that raises the wave
 // most 4); the flat-tail rescue done / its relaxed acceptance pending
 // the polish phase: F in the cancellation-free form from here on / its
 // re-evaluation at u pending
+// the gradient fallback: its line search running / its re-evaluation at u
+// pending, and its count (kEscGradCount, in units of kEscGradN: at most 8)
 constexpr unsigned kEscIndef = 1u, kEscProbe = 2u, kEscNc = 4u, kEscExhOk = 8u, kEscN = 16u, kEscCount = 0x70u,
-                   kEscRescued = 0x100u, kEscRelax = 0x200u, kEscPolish = 0x400u, kEscPolishProbe = 0x800u;
+                   kEscRescued = 0x100u, kEscRelax = 0x200u, kEscPolish = 0x400u, kEscPolishProbe = 0x800u,
+                   kEscGrad = 0x1000u, kEscGradProbe = 0x2000u, kEscGradN = 0x4000u, kEscGradCount = 0x3C000u;
 
 // ---------------------------------------------------------------------------
 // The predictive HPDI's per-position step (K4a, and the fused prep of the PPL-1
@@ -495,8 +498,10 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       // the polish phase's re-evaluation at u (F now in the other form): taken
       // as the current point, then the ordinary Newton step (the same d)
       const bool pprobe = esc & kEscPolishProbe;
-      esc &= ~(kEscProbe | kEscPolishProbe);
-      if (probed || pprobe) {
+      // the gradient fallback's re-evaluation at u: its g gives the direction
+      const bool gprobe = esc & kEscGradProbe;
+      esc &= ~(kEscProbe | kEscPolishProbe | kEscGradProbe);
+      if (probed || pprobe || gprobe) {
         accept = true;
       } else if (first) {
         accept = true;
@@ -517,15 +522,31 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         curF = tr.F;
         curMag = tr.mag;
         curPg = pgt;
-        esc &= ~kEscNc;
+        esc &= ~(kEscNc | kEscGrad);
         if (!done) {
+          // (the gradient fallback's probe: the projected-gradient direction
+          // replaces the Newton step; oracle: fit_one)
           const bool ind = newton_dir(pa.pmd, u, tr.g, tr.H, pgt, d, probed);
+          const bool gok = gprobe && pg_direction(u, tr.g, d);
           curG3 = tr.g[3];
           curGd = tr.g[0] * d[0] + tr.g[1] * d[1] + tr.g[2] * d[2] + tr.g[3] * d[3];
           t = 1.0;
-          if (probed) {
+          if (gprobe) {
+            if (gok) {
+              esc |= kEscNc | kEscGrad;
+            } else {
+              done = true;
+              status = (esc & kEscExhOk) ? MDFIT_OK : MDFIT_MAXITER;
+            }
+          } else if (probed) {
             if (ind) {
               esc += kEscN | kEscNc;
+            } else if (!(esc & kEscExhOk) && (esc & kEscGradCount) < 8u * kEscGradN && evals < max_iter) {
+              // no escape direction: the gradient fallback, from its own
+              // re-evaluation at u (oracle: fit_one)
+              esc += kEscGradN;
+              esc |= kEscGradProbe;
+              d[0] = d[1] = d[2] = d[3] = 0.0;
             } else {
               done = true;
               status = (esc & kEscExhOk) ? MDFIT_OK : MDFIT_MAXITER;
@@ -540,9 +561,21 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         }
       } else if (esc & kEscNc) {  // the escape finds no decrease beyond F's rounding
         t *= 0.5;
-        if (t < 1e-3) {
-          done = true;
-          status = (esc & kEscExhOk) ? MDFIT_OK : MDFIT_MAXITER;
+        if (t < ((esc & kEscGrad) ? 1e-6 : 1e-3)) {
+          if (esc & kEscGrad) {
+            // nor does the projected gradient, for steps down to 1e-6: optimal
+            // to F's resolution (oracle: fit_one)
+            done = true;
+            status = MDFIT_OK;
+          } else if (!(esc & kEscExhOk) && (esc & kEscGradCount) < 8u * kEscGradN && evals < max_iter) {
+            esc += kEscGradN;  // the gradient fallback: re-evaluate at u next trip
+            esc |= kEscGradProbe;
+            d[0] = d[1] = d[2] = d[3] = 0.0;
+            t = 1.0;
+          } else {
+            done = true;
+            status = (esc & kEscExhOk) ? MDFIT_OK : MDFIT_MAXITER;
+          }
         }
       } else {
         t *= 0.5;
@@ -571,6 +604,12 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
             if ((esc & kEscIndef) && (esc & kEscCount) < 4u * kEscN && evals < max_iter) {
               // the saddle escape (oracle: fit_one): re-evaluate at u next trip
               esc |= kEscProbe;
+              d[0] = d[1] = d[2] = d[3] = 0.0;
+              t = 1.0;
+            } else if (!exh_ok && (esc & kEscGradCount) < 8u * kEscGradN && evals < max_iter) {
+              // the gradient fallback (oracle: fit_one): re-evaluate at u next trip
+              esc += kEscGradN;
+              esc |= kEscGradProbe;
               d[0] = d[1] = d[2] = d[3] = 0.0;
               t = 1.0;
             } else {

@@ -337,6 +337,19 @@ __device__ __forceinline__ double pgnorm(const double u[4], const double g[4]) {
   return m;
 }
 
+// the projected-gradient direction P(u - g) - u scaled to max-norm 1 (the
+// gradient fallback of fit_kernel; oracle: pg_direction); false when it vanishes
+__device__ __forceinline__ bool pg_direction(const double u[4], const double g[4], double d[4]) {
+  double p[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) p[j] = clampd(u[j] - g[j], kULo[j], kUHi[j]) - u[j];
+  const double mx = maxabs4(p);
+  if (!(mx > 0.0)) return false;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) d[j] = p[j] / mx;
+  return true;
+}
+
 constexpr double kEpsBind[4] = {1e-3, 1e-3, 1e-4, 1e-3};
 
 // 1/sqrt(x), x > 0: v_rsq_f64 + two Newton steps (no IEEE sqrt sequence)

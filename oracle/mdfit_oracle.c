@@ -465,6 +465,17 @@ static double pgnorm(const double u[4], const double g[4]) {
   return m;
 }
 
+/* the projected-gradient direction P(u - g) - u scaled to max-norm 1 (the
+ * gradient fallback below); 0 when the projected gradient vanishes */
+static int pg_direction(const double u[4], const double g[4], double v[4]) {
+  double p[4];
+  for (int j = 0; j < 4; j++) p[j] = clampd(u[j] - g[j], U_LO[j], U_HI[j]) - u[j];
+  const double mx = maxabs4(p);
+  if (!(mx > 0)) return 0;
+  for (int j = 0; j < 4; j++) v[j] = p[j] / mx;
+  return 1;
+}
+
 
 typedef struct {
   double u[4];
@@ -499,6 +510,7 @@ static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
   }
   int rescued = 0, relax = 0; /* the flat-tail rescue (below): once per fit */
   int nc = 0, n_nc = 0, st_exh = MDFIT_MAXITER; /* the saddle escape (below) */
+  int grad = 0, n_grad = 0;                       /* the gradient fallback (below): up to 8 times per fit */
   while (evals < max_iter) {
     for (int j = 0; j < 4; j++) ut[j] = clampd(u[j] + t * d[j], U_LO[j], U_HI[j]);
     evaluate(model, y, N, lo, hi, ut, &tr, accf);
@@ -517,7 +529,7 @@ static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
       memcpy(u, ut, sizeof(u));
       cur = tr;
       indef = direction(model, u, cur.g, cur.H, d);
-      nc = 0;
+      nc = grad = 0;
       t = 1.0;
       if (maxabs4(d) <= tol) {
         status = MDFIT_OK;
@@ -525,7 +537,30 @@ static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
       }
     } else if (nc) { /* the escape step finds no decrease beyond F's rounding */
       t *= 0.5;
-      if (t < 1e-3) {
+      if (t < (grad ? 1e-6 : 1e-3)) {
+        /* no decrease beyond F's rounding along the projected gradient either,
+         * for steps down to 1e-6: optimal to F's resolution (the boundary fits
+         * at c -> 0 whose curvature in c grows by ~1e7 within 1e-6 of the bound) */
+        if (grad) {
+          status = MDFIT_OK;
+          break;
+        }
+        /* the gradient fallback: a fit that ends here unconverged (an escape
+         * direction or the Newton step pushing a variable that sits on its
+         * bound outward, while the gradient pulls it inward -- every clamped
+         * trial then raises F) tries (up to 8 times per fit) the projected-gradient direction
+         * P(u - g) - u, re-evaluating at u first as the kernel does, with the
+         * escape's strict acceptance, halving to 1e-6 */
+        if (st_exh != MDFIT_OK && n_grad < 8 && evals < max_iter) {
+          evaluate(model, y, N, lo, hi, u, &tr, accf);
+          evals++;
+          n_grad++;
+          if (pg_direction(u, tr.g, d)) {
+            grad = 1;
+            t = 1.0;
+            continue;
+          }
+        }
         status = st_exh;
         break;
       }
@@ -582,6 +617,16 @@ static void fit_one(int model, const uint32_t* y, const uint32_t* N, int lo,
           if (nc_direction(model, u, tr.g, tr.H, d)) {
             n_nc++;
             nc = 1;
+            t = 1.0;
+            continue;
+          }
+        }
+        if (st_exh != MDFIT_OK && n_grad < 8 && evals < max_iter) { /* the gradient fallback (above) */
+          evaluate(model, y, N, lo, hi, u, &tr, accf);
+          evals++;
+          n_grad++;
+          if (pg_direction(u, tr.g, d)) {
+            nc = grad = 1;
             t = 1.0;
             continue;
           }
