@@ -55,15 +55,6 @@ int64_t mdi_n_strings(const mdi_table* t, int which);
 int64_t mdi_string_bytes(const mdi_table* t, int which);
 int mdi_strings(const mdi_table* t, int which, char* buf, int64_t* offsets);
 
-/* The same parse with the 16 count columns as uint32 (counts16 =
- * uint32_t[16][rows]): *wide = 1 when some count lies outside [0, 2^32) --
- * the caller then parses the file again with mdi_parse_into (int64), so the
- * result never depends on the narrowing.  Half the bytes written and re-read
- * by the count pipeline (mdi_select_u32 / mdi_gather_u32) for the usual file. */
-int mdi_parse_into_u32(mdi_table* t, int64_t* tax_id, int64_t* n_alignments, int64_t* position,
-                       uint32_t* counts16, int32_t* name_code, int32_t* rank_code, int32_t* strand_code,
-                       int* wide);
-
 void mdi_free(mdi_table* t);
 const char* mdi_last_error(void);
 
@@ -87,13 +78,6 @@ int64_t mdi_select(int64_t rows, const int64_t* tax_id, const int64_t* n_alignme
                    int64_t min_y_sum, int n_threads, int32_t* taxon, int64_t* y_sum_total, int64_t* perm,
                    int64_t* uniq, int64_t* n_taxa);
 
-/* mdi_select over uint32 count columns (mdi_parse_into_u32) */
-int64_t mdi_select_u32(int64_t rows, const int64_t* tax_id, const int64_t* n_alignments, const int64_t* position,
-                       const uint32_t* counts16, const int32_t* strand_code, const uint8_t* code_is_fwd,
-                       int32_t n_codes, const char* sub_fwd, const char* sub_rev, int64_t min_alignments,
-                       int64_t min_y_sum, int n_threads, int32_t* taxon, int64_t* y_sum_total, int64_t* perm,
-                       int64_t* uniq, int64_t* n_taxa);
-
 /* mdi_gather writes the numeric columns of the counts table for the rows
  * perm[0..n_keep), downcast as utils.py:329-356 (add_reference_counts,
  * add_error_rates, positions: counts.py:86-126): N_alignments, position
@@ -107,13 +91,6 @@ int mdi_gather(int64_t rows, const int64_t* perm, int64_t n_keep, const int64_t*
                const uint8_t* code_is_fwd, int32_t n_codes, const char* sub_fwd, const char* sub_rev,
                const int64_t* y_sum_total, int n_threads, uint32_t* o_nal, int8_t* o_position,
                uint32_t* o_counts16, uint32_t* o_ref2, float* o_f2, uint32_t* o_y_sum_total);
-
-/* mdi_gather over uint32 count columns (mdi_parse_into_u32) */
-int mdi_gather_u32(int64_t rows, const int64_t* perm, int64_t n_keep, const int64_t* n_alignments,
-                   const int64_t* position, const uint32_t* counts16, const int32_t* strand_code,
-                   const uint8_t* code_is_fwd, int32_t n_codes, const char* sub_fwd, const char* sub_rev,
-                   const int64_t* y_sum_total, int n_threads, uint32_t* o_nal, int8_t* o_position,
-                   uint32_t* o_counts16, uint32_t* o_ref2, float* o_f2, uint32_t* o_y_sum_total);
 
 /* mdi_noise: add_noise_estimates (fits.py:359-376) of n_taxa packed taxa on
  * the host, so the 1,440 B/taxon of mismatch counts need not cross PCIe:

@@ -31,19 +31,16 @@
 
 namespace {
 
-// C: the count columns' type -- int64 (mdi_parse_into) or uint32
-// (mdi_parse_into_u32, a file whose counts all fit)
-template <typename C>
 struct Rows {
   int64_t n;
   const int64_t* tax_id;
   const int64_t* nal;
   const int64_t* position;
-  const C* counts;  // [16][n]
+  const int64_t* counts;  // [16][n]
   const int32_t* strand_code;
   const uint8_t* code_is_fwd;
   int n_codes;
-  const C* col(int k) const { return counts + (int64_t)k * n; }
+  const int64_t* col(int k) const { return counts + (int64_t)k * n; }
   bool fwd(int64_t r) const {
     const int32_t c = strand_code[r];
     return c >= 0 && c < n_codes && code_is_fwd[c];
@@ -91,12 +88,10 @@ int arg_error(const char* what) {
 
 }  // namespace
 
-namespace {
+extern "C" {
 
-
-template <typename C>
-int64_t select_impl(int64_t rows, const int64_t* tax_id, const int64_t* n_alignments, const int64_t* position,
-                   const C* counts16, const int32_t* strand_code, const uint8_t* code_is_fwd,
+int64_t mdi_select(int64_t rows, const int64_t* tax_id, const int64_t* n_alignments, const int64_t* position,
+                   const int64_t* counts16, const int32_t* strand_code, const uint8_t* code_is_fwd,
                    int32_t n_codes, const char* sub_fwd, const char* sub_rev, int64_t min_alignments,
                    int64_t min_y_sum, int n_threads, int32_t* taxon, int64_t* y_sum_total, int64_t* perm,
                    int64_t* uniq, int64_t* n_taxa) {
@@ -106,9 +101,9 @@ int64_t select_impl(int64_t rows, const int64_t* tax_id, const int64_t* n_alignm
     return arg_error("mdi_select: bad arguments");
   const int kf = pair_index(sub_fwd), kr = pair_index(sub_rev);
   if (kf < 0 || kr < 0) return arg_error("mdi_select: substitutions must be base pairs like \"CT\"");
-  const Rows<C> R{rows, tax_id, n_alignments, position, counts16, strand_code, code_is_fwd, n_codes};
-  const C* yf = R.col(kf);
-  const C* yr = R.col(kr);
+  const Rows R{rows, tax_id, n_alignments, position, counts16, strand_code, code_is_fwd, n_codes};
+  const int64_t* yf = R.col(kf);
+  const int64_t* yr = R.col(kr);
   const int nt = pool_size(n_threads, rows);
 
   // (1) per row range: the runs of equal tax_id and their substitution sums
@@ -121,7 +116,7 @@ int64_t select_impl(int64_t rows, const int64_t* tax_id, const int64_t* n_alignm
     for (int64_t r = lo; r < hi; ++r) {
       if (r == lo || tax_id[r] != tax_id[r - 1]) v.push_back({r, tax_id[r], 0});
       const int64_t p = R.pos(r);
-      v.back().ys += p > 0 ? (int64_t)yf[r] : (p < 0 ? (int64_t)yr[r] : 0);
+      v.back().ys += p > 0 ? yf[r] : (p < 0 ? yr[r] : 0);
     }
   });
   // (2) taxon index in first-appearance order (pd.factorize) over the runs, in file order
@@ -243,9 +238,8 @@ int64_t select_impl(int64_t rows, const int64_t* tax_id, const int64_t* n_alignm
   return n_keep;
 }
 
-template <typename C>
-int gather_impl(int64_t rows, const int64_t* perm, int64_t n_keep, const int64_t* n_alignments,
-               const int64_t* position, const C* counts16, const int32_t* strand_code,
+int mdi_gather(int64_t rows, const int64_t* perm, int64_t n_keep, const int64_t* n_alignments,
+               const int64_t* position, const int64_t* counts16, const int32_t* strand_code,
                const uint8_t* code_is_fwd, int32_t n_codes, const char* sub_fwd, const char* sub_rev,
                const int64_t* y_sum_total, int n_threads, uint32_t* o_nal, int8_t* o_position,
                uint32_t* o_counts16, uint32_t* o_ref2, float* o_f2, uint32_t* o_y_sum_total) {
@@ -255,7 +249,7 @@ int gather_impl(int64_t rows, const int64_t* perm, int64_t n_keep, const int64_t
     return arg_error("mdi_gather: bad arguments");
   const int kf = pair_index(sub_fwd), kr = pair_index(sub_rev);
   if (kf < 0 || kr < 0) return arg_error("mdi_gather: substitutions must be base pairs like \"CT\"");
-  const Rows<C> R{rows, nullptr, n_alignments, position, counts16, strand_code, code_is_fwd, n_codes};
+  const Rows R{rows, nullptr, n_alignments, position, counts16, strand_code, code_is_fwd, n_codes};
   const int ref_base[2] = {kf / 4, kr / 4};
   const int sub[2] = {kf, kr};
   int nt = n_threads > 0 ? n_threads : mdi_default_threads();
@@ -279,8 +273,7 @@ int gather_impl(int64_t rows, const int64_t* perm, int64_t n_keep, const int64_t
       }
       for (int s = 0; s < 2; ++s) {
         const int b = ref_base[s];
-        const int64_t ref = (int64_t)R.col(4 * b)[r] + (int64_t)R.col(4 * b + 1)[r] + (int64_t)R.col(4 * b + 2)[r] +
-                            (int64_t)R.col(4 * b + 3)[r];
+        const int64_t ref = R.col(4 * b)[r] + R.col(4 * b + 1)[r] + R.col(4 * b + 2)[r] + R.col(4 * b + 3)[r];
         ovf |= ref > big;
         o_ref2[(int64_t)s * n_keep + i] = (uint32_t)ref;
         const int64_t c = R.col(sub[s])[r];
@@ -308,48 +301,6 @@ int gather_impl(int64_t rows, const int64_t* perm, int64_t n_keep, const int64_t
       return MDI_E_RANGE;
     }
   return 0;
-}
-
-}  // namespace
-
-extern "C" {
-
-int64_t mdi_select(int64_t rows, const int64_t* tax_id, const int64_t* n_alignments, const int64_t* position,
-                   const int64_t* counts16, const int32_t* strand_code, const uint8_t* code_is_fwd,
-                   int32_t n_codes, const char* sub_fwd, const char* sub_rev, int64_t min_alignments,
-                   int64_t min_y_sum, int n_threads, int32_t* taxon, int64_t* y_sum_total, int64_t* perm,
-                   int64_t* uniq, int64_t* n_taxa) {
-  return select_impl(rows, tax_id, n_alignments, position, counts16, strand_code, code_is_fwd, n_codes, sub_fwd,
-                     sub_rev, min_alignments, min_y_sum, n_threads, taxon, y_sum_total, perm, uniq, n_taxa);
-}
-
-int64_t mdi_select_u32(int64_t rows, const int64_t* tax_id, const int64_t* n_alignments, const int64_t* position,
-                       const uint32_t* counts16, const int32_t* strand_code, const uint8_t* code_is_fwd,
-                       int32_t n_codes, const char* sub_fwd, const char* sub_rev, int64_t min_alignments,
-                       int64_t min_y_sum, int n_threads, int32_t* taxon, int64_t* y_sum_total, int64_t* perm,
-                       int64_t* uniq, int64_t* n_taxa) {
-  return select_impl(rows, tax_id, n_alignments, position, counts16, strand_code, code_is_fwd, n_codes, sub_fwd,
-                     sub_rev, min_alignments, min_y_sum, n_threads, taxon, y_sum_total, perm, uniq, n_taxa);
-}
-
-int mdi_gather(int64_t rows, const int64_t* perm, int64_t n_keep, const int64_t* n_alignments,
-               const int64_t* position, const int64_t* counts16, const int32_t* strand_code,
-               const uint8_t* code_is_fwd, int32_t n_codes, const char* sub_fwd, const char* sub_rev,
-               const int64_t* y_sum_total, int n_threads, uint32_t* o_nal, int8_t* o_position,
-               uint32_t* o_counts16, uint32_t* o_ref2, float* o_f2, uint32_t* o_y_sum_total) {
-  return gather_impl(rows, perm, n_keep, n_alignments, position, counts16, strand_code, code_is_fwd, n_codes,
-                     sub_fwd, sub_rev, y_sum_total, n_threads, o_nal, o_position, o_counts16, o_ref2, o_f2,
-                     o_y_sum_total);
-}
-
-int mdi_gather_u32(int64_t rows, const int64_t* perm, int64_t n_keep, const int64_t* n_alignments,
-                   const int64_t* position, const uint32_t* counts16, const int32_t* strand_code,
-                   const uint8_t* code_is_fwd, int32_t n_codes, const char* sub_fwd, const char* sub_rev,
-                   const int64_t* y_sum_total, int n_threads, uint32_t* o_nal, int8_t* o_position,
-                   uint32_t* o_counts16, uint32_t* o_ref2, float* o_f2, uint32_t* o_y_sum_total) {
-  return gather_impl(rows, perm, n_keep, n_alignments, position, counts16, strand_code, code_is_fwd, n_codes,
-                     sub_fwd, sub_rev, y_sum_total, n_threads, o_nal, o_position, o_counts16, o_ref2, o_f2,
-                     o_y_sum_total);
 }
 
 const char* mdi_counts_error(void) { return g_cerr; }

@@ -64,7 +64,6 @@ struct Chunk {
   int64_t row0 = 0, rows = 0;  // rows: non-blank lines
   LocalStrings str[3];
   int err = 0;
-  int wide = 0;  // (u32 counts) a count outside [0, 2^32): the caller re-parses in int64
   long bad_row = 0;
   int bad_col = 0;
 };
@@ -175,19 +174,15 @@ int64_t count_rows(const char* p, const char* end) {
   return n;
 }
 
-// C: the count columns' type (int64, or uint32 with the wide flag)
-template <typename C>
 struct Out {
-  int64_t *tax_id, *nal, *pos;
-  C* counts;
+  int64_t *tax_id, *nal, *pos, *counts;
   int32_t* code[3];
   int64_t rows;
   const char* map_end;  // readable bytes of the mapping end here
 };
 
 // one line [p, its '\n'] into row r; false on a malformed field (col set)
-template <typename C>
-inline bool parse_line(const char*& p, const char* lim, int format, const Out<C>& o, Chunk* c, int64_t r, int& col) {
+inline bool parse_line(const char*& p, const char* lim, int format, const Out& o, Chunk* c, int64_t r, int& col) {
   col = 0;
   int64_t tid, nal, pos;
   int32_t name = 0, rank = 0;
@@ -214,8 +209,7 @@ inline bool parse_line(const char*& p, const char* lim, int format, const Out<C>
   for (int j = 0; j < 16; ++j) {  // column-major: counts[j][rows]
     int64_t v;
     if (!tab(p) || !parse_int(p, lim, &v)) return false;
-    if (sizeof(C) == 4) c->wide |= (uint64_t)v > 0xFFFFFFFFull;
-    o.counts[(int64_t)j * o.rows + r] = (C)v;
+    o.counts[(int64_t)j * o.rows + r] = v;
     ++col;
   }
   while (*p == '\r') ++p;
@@ -230,8 +224,7 @@ inline bool parse_line(const char*& p, const char* lim, int format, const Out<C>
   return true;
 }
 
-template <typename C>
-void parse_chunk(Chunk* c, int format, const Out<C>& o) {
+void parse_chunk(Chunk* c, int format, const Out& o) {
   const char* p = c->begin;
   const char* end = c->end;
   int64_t r = c->row0;
@@ -369,23 +362,15 @@ int mdi_open(const char* path, int n_threads, mdi_table** out) {
 int mdi_format(const mdi_table* t) { return t ? t->format : MDI_E_ARG; }
 int64_t mdi_rows(const mdi_table* t) { return t ? t->rows : MDI_E_ARG; }
 
-}  // extern "C"
-
-namespace {
-template <typename C>
-int parse_into(mdi_table* t, int64_t* tax_id, int64_t* n_alignments, int64_t* position, C* counts16,
-               int32_t* name_code, int32_t* rank_code, int32_t* strand_code, int* wide) {
+int mdi_parse_into(mdi_table* t, int64_t* tax_id, int64_t* n_alignments, int64_t* position, int64_t* counts16,
+                   int32_t* name_code, int32_t* rank_code, int32_t* strand_code) {
   if (!t || !tax_id || !n_alignments || !position || !counts16 || !name_code || !rank_code || !strand_code)
     return fail(MDI_E_ARG, "null argument");
   if (t->parsed) return fail(MDI_E_ARG, "table already parsed");
-  const Out<C> o{tax_id, n_alignments, position, counts16, {name_code, rank_code, strand_code}, t->rows,
-                 (const char*)t->map + t->size};
+  const Out o{tax_id, n_alignments, position, counts16, {name_code, rank_code, strand_code}, t->rows,
+              (const char*)t->map + t->size};
   const int format = t->format;
   parallel_chunks(t->chunks, [&](size_t i) { parse_chunk(&t->chunks[i], format, o); });
-  if (wide) {
-    *wide = 0;
-    for (const Chunk& c : t->chunks) *wide |= c.wide;
-  }
   for (const Chunk& c : t->chunks)
     if (c.err) {  // line number of the malformed row: count lines before its chunk
       long line = t->first_line;
@@ -426,20 +411,6 @@ int parse_into(mdi_table* t, int64_t* tax_id, int64_t* n_alignments, int64_t* po
   t->parsed = true;
   g_err[0] = '\0';
   return 0;
-}
-}  // namespace
-
-extern "C" {
-
-int mdi_parse_into(mdi_table* t, int64_t* tax_id, int64_t* n_alignments, int64_t* position, int64_t* counts16,
-                   int32_t* name_code, int32_t* rank_code, int32_t* strand_code) {
-  return parse_into(t, tax_id, n_alignments, position, counts16, name_code, rank_code, strand_code, nullptr);
-}
-
-int mdi_parse_into_u32(mdi_table* t, int64_t* tax_id, int64_t* n_alignments, int64_t* position, uint32_t* counts16,
-                       int32_t* name_code, int32_t* rank_code, int32_t* strand_code, int* wide) {
-  if (!wide) return fail(MDI_E_ARG, "null argument");
-  return parse_into(t, tax_id, n_alignments, position, counts16, name_code, rank_code, strand_code, wide);
 }
 
 int64_t mdi_n_strings(const mdi_table* t, int which) {

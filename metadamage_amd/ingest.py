@@ -39,8 +39,6 @@ def _load():
         lib.mdi_open.restype = ctypes.c_int
         lib.mdi_parse_into.argtypes = [vp] + [vp] * 7
         lib.mdi_parse_into.restype = ctypes.c_int
-        lib.mdi_parse_into_u32.argtypes = [vp] + [vp] * 8
-        lib.mdi_parse_into_u32.restype = ctypes.c_int
         lib.mdi_format.argtypes = [vp]
         lib.mdi_format.restype = ctypes.c_int
         lib.mdi_rows.argtypes = [vp]
@@ -57,13 +55,9 @@ def _load():
         lib.mdi_select.argtypes = [i64, vp, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_char_p, ctypes.c_char_p,
                                    i64, i64, ctypes.c_int, vp, vp, vp, vp, vp]
         lib.mdi_select.restype = i64
-        lib.mdi_select_u32.argtypes = lib.mdi_select.argtypes
-        lib.mdi_select_u32.restype = i64
         lib.mdi_gather.argtypes = [i64, vp, i64, vp, vp, vp, vp, vp, ctypes.c_int32, ctypes.c_char_p,
                                    ctypes.c_char_p, vp, ctypes.c_int, vp, vp, vp, vp, vp, vp]
         lib.mdi_gather.restype = ctypes.c_int
-        lib.mdi_gather_u32.argtypes = lib.mdi_gather.argtypes
-        lib.mdi_gather_u32.restype = ctypes.c_int
         lib.mdi_counts_error.restype = ctypes.c_char_p
         lib.mdi_codes.argtypes = [i64, vp, ctypes.c_int, vp, vp, ctypes.c_int, vp, vp]
         lib.mdi_codes.restype = ctypes.c_int
@@ -125,7 +119,7 @@ class Table:
     tax_id: np.ndarray  # int64[rows]
     n_alignments: np.ndarray
     position: np.ndarray  # as in the file (0-indexed)
-    counts: np.ndarray  # int64[16][rows] (uint32 from read_table(narrow=True)), AA .. TT
+    counts: np.ndarray  # int64[16][rows], AA .. TT
     name_code: np.ndarray  # int32[rows] into names
     names: np.ndarray  # object[n]
     rank_code: np.ndarray
@@ -155,12 +149,10 @@ def _scratch(name: str, shape, dtype) -> np.ndarray:
     return a[:n].reshape(shape)
 
 
-def read_table(path, n_threads: int = 0, scratch: bool = False, narrow: bool = False) -> Table | None:
+def read_table(path, n_threads: int = 0, scratch: bool = False) -> Table:
     """Parse a count table with the native reader.  scratch: the numeric
     columns live in this thread's reused buffers (valid until its next
-    scratch call; compute_counts).  narrow: the 16 count columns as uint32
-    (mdi_parse_into_u32); None when some count does not fit (parse again
-    without)."""
+    scratch call; compute_counts)."""
     lib = _load()
     h = ctypes.c_void_p()
     rc = lib.mdi_open(os.fsencode(str(path)), int(n_threads), ctypes.byref(h))
@@ -170,20 +162,12 @@ def read_table(path, n_threads: int = 0, scratch: bool = False, narrow: bool = F
     try:
         n = int(lib.mdi_rows(h))
         cols = [alloc(f"col{i}", n, np.int64) for i in range(3)]
-        # column-major: one contiguous array per base pair
-        counts = alloc("counts32" if narrow else "counts", (16, n), np.uint32 if narrow else np.int64)
+        counts = alloc("counts", (16, n), np.int64)  # column-major: one contiguous array per base pair
         codes = [alloc(f"code{i}", n, np.int32) for i in range(3)]
         # (no pre-fault: the parser threads first-touch their own row ranges in
         # parallel -- faulting ~470 MB here on one thread cost more than the parse)
-        if narrow:
-            wide = ctypes.c_int(0)
-            rc = lib.mdi_parse_into_u32(h, *(c.ctypes.data for c in cols), counts.ctypes.data,
-                                        *(c.ctypes.data for c in codes), ctypes.byref(wide))
-            if rc == 0 and wide.value:
-                return None
-        else:
-            rc = lib.mdi_parse_into(h, *(c.ctypes.data for c in cols), counts.ctypes.data,
-                                    *(c.ctypes.data for c in codes))
+        rc = lib.mdi_parse_into(h, *(c.ctypes.data for c in cols), counts.ctypes.data,
+                                *(c.ctypes.data for c in codes))
         if rc != 0:
             raise ValueError(f"{path}: {lib.mdi_last_error().decode()}")
         tables = []
@@ -289,17 +273,7 @@ def compute_counts(cfg, table: Table | None = None, n_threads: int = 0) -> pd.Da
     csrc/counts.cpp); the categoricals from the interned string codes.  Same
     frame as compute_counts_numpy and counts.compute_counts_pandas."""
     lib = _load()
-    if table is None:
-        # uint32 counts (half the bytes through the pipeline) unless a count
-        # does not fit, then the int64 parse -- the same frame either way
-        t = read_table(cfg.filename, n_threads, scratch=True, narrow=True)
-        if t is None:
-            t = read_table(cfg.filename, n_threads, scratch=True)
-    else:
-        t = table
-    u32 = t.counts.dtype == np.uint32
-    select = lib.mdi_select_u32 if u32 else lib.mdi_select
-    gather = lib.mdi_gather_u32 if u32 else lib.mdi_gather
+    t = read_table(cfg.filename, n_threads, scratch=True) if table is None else table
     fwd, rev = cfg.substitution_bases_forward, cfg.substitution_bases_reverse
     n = t.rows
     is_fwd = np.ascontiguousarray(t.strands == "5'", dtype=np.uint8)
@@ -310,7 +284,7 @@ def compute_counts(cfg, table: Table | None = None, n_threads: int = 0) -> pd.Da
               len(is_fwd), fwd.encode(), rev.encode())
     uniq = _scratch("uniq", n, np.int64)
     n_taxa = ctypes.c_int64(0)
-    k = select(n, t.tax_id.ctypes.data, t.n_alignments.ctypes.data, *common, int(cfg.min_alignments),
+    k = lib.mdi_select(n, t.tax_id.ctypes.data, t.n_alignments.ctypes.data, *common, int(cfg.min_alignments),
                        int(cfg.min_y_sum), int(n_threads), taxon.ctypes.data, ysum.ctypes.data, perm.ctypes.data,
                        uniq.ctypes.data, ctypes.byref(n_taxa))
     if k < 0:
@@ -323,7 +297,7 @@ def compute_counts(cfg, table: Table | None = None, n_threads: int = 0) -> pd.Da
     ref2 = np.empty((2, k), np.uint32)
     f2 = np.empty((2, k), np.float32)
     ys = np.empty(k, np.uint32)
-    rc = gather(n, perm.ctypes.data, k, t.n_alignments.ctypes.data, *common, ysum.ctypes.data,
+    rc = lib.mdi_gather(n, perm.ctypes.data, k, t.n_alignments.ctypes.data, *common, ysum.ctypes.data,
                         int(n_threads), nal.ctypes.data, pos.ctypes.data, c16.ctypes.data, ref2.ctypes.data,
                         f2.ctypes.data, ys.ctypes.data)
     if rc != 0:

@@ -358,26 +358,3 @@ def test_native_noise_matches_the_reference_restatement():
     assert np.array_equal(np.isnan(nz), np.isnan(ref))
     ok = ~np.isnan(ref)
     assert (np.abs(nz[ok] - ref[ok]) <= 1e-13 * np.abs(ref[ok])).all()
-
-
-def test_native_reader_u32_counts(tmp_path):
-    """The uint32 parse (mdi_parse_into_u32) holds the int64 parse's counts,
-    and a file with a count outside [0, 2^32) reports itself wide (None) --
-    compute_counts then parses it in int64 (test_native_pipeline_uint32_overflow)."""
-    from metadamage_amd import ingest
-    from metadamage_amd.synthetic import generate, to_counts_table
-
-    table = to_counts_table(generate(300, seed=35))
-    f = tmp_path / "t.tsv"
-    table.to_csv(f, sep="\t", header=False, index=False)
-    a, b = ingest.read_table(f, 2), ingest.read_table(f, 2, narrow=True)
-    assert b.counts.dtype == np.uint32 and np.array_equal(a.counts, b.counts.astype(np.int64))
-    for k in ("tax_id", "n_alignments", "position", "name_code", "strand_code"):
-        assert np.array_equal(getattr(a, k), getattr(b, k)), k
-    for bad in (2**32, -1):
-        t2 = table.copy()
-        t2.iloc[7, 9] = bad
-        g = tmp_path / f"w{bad}.tsv"
-        t2.to_csv(g, sep="\t", header=False, index=False)
-        assert ingest.read_table(g, 2, narrow=True) is None
-        assert int(ingest.read_table(g, 2).counts[3, 7]) == bad
