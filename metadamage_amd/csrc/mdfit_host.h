@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 
 #include "../../include/mdfit.h"
 
@@ -27,9 +29,10 @@ void prof_mark(int slot, hipStream_t s);
 // persistent grid: no more waves than can be resident at once (so every
 // wave starts immediately and pulls work until its queue is drained), a
 // multiple of the 8 queues
-// (cap_per_cu > 0: at most that many waves per CU -- development A/B)
+// (cap_per_cu > 0: at most that many waves per CU; force_per_cu > 0: exactly
+// that many -- development A/B; MDFIT_DEV_GRID prints the sizing)
 template <typename K>
-int64_t fit_grid(K kernel, int64_t ntask, int fits_per_wave, int cap_per_cu = 0) {
+int64_t fit_grid(K kernel, int64_t ntask, int fits_per_wave, int cap_per_cu = 0, int force_per_cu = 0) {
   int dev = 0, n_cu = 256, per_cu = 8;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
@@ -37,10 +40,20 @@ int64_t fit_grid(K kernel, int64_t ntask, int fits_per_wave, int cap_per_cu = 0)
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kWave, 0) != hipSuccess || per_cu <= 0)
     per_cu = 8;
   if (cap_per_cu > 0 && cap_per_cu < per_cu) per_cu = cap_per_cu;
+  const int api = per_cu;
+  if (force_per_cu > 0) per_cu = force_per_cu;
   const int64_t want = (ntask + fits_per_wave - 1) / fits_per_wave;
   const int64_t cap = (int64_t)n_cu * per_cu;
   int64_t g = want < cap ? want : cap;
   g = ((g + kQueues - 1) / kQueues) * kQueues;
+  if (std::getenv("MDFIT_DEV_GRID")) {
+    hipFuncAttributes fa{};
+    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kernel));
+    int lds_cu = 0;
+    (void)hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev);
+    std::fprintf(stderr, "fit_grid: n_cu %d occupancy-api %d per_cu %d lds/block %zu regs %d lds/cu %d -> grid %lld\n",
+                 n_cu, api, per_cu, fa.sharedSizeBytes, fa.numRegs, lds_cu, (long long)g);
+  }
   return g < kQueues ? kQueues : g;
 }
 }  // namespace mdfit::host

@@ -1471,7 +1471,11 @@ int fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t 
   if (hipMemsetAsync(out, 0, (size_t)n_taxa * MDFIT_NOUT * sizeof(double), s) != hipSuccess)
     return host::check_launch("hipMemsetAsync(out)");
   constexpr int kPPL = MDFIT_NUTS_PPL;
-  const int64_t g = host::fit_grid(nuts_chain_kernel<kPPL>, 4 * n_taxa, kPPL == 1 ? 2 : 4);
+  // (MDFIT_DEV_PER_CU: waves per CU forced, development A/B; the chain
+  // kernel's waves never wait on each other, so any grid drains)
+  const char* force = std::getenv("MDFIT_DEV_PER_CU");
+  const int64_t g =
+      host::fit_grid(nuts_chain_kernel<kPPL>, 4 * n_taxa, kPPL == 1 ? 2 : 4, 0, force ? std::atoi(force) : 0);
   host::prof_mark(1, s);
   hipLaunchKernelGGL(nuts_chain_kernel<kPPL>, dim3((unsigned)g), dim3(kWave), 0, s, y, N, n_taxa, o, out, ws,
                      samples);
