@@ -80,6 +80,13 @@ __device__ __forceinline__ Stream make_stream(uint64_t seed, int64_t g, int sub)
 
 __device__ __forceinline__ uint4 block(const Stream& s, uint32_t w2, uint32_t w3) {
   uint32_t c0 = s.c0, c1 = s.c1, c2 = w2, c3 = w3, k0 = s.k0, k1 = s.k1;
+  // The key is the seed in every stream (make_stream), so it is wave-uniform:
+  // held in SGPRs and opaque here, so the round-key schedule is recomputed on
+  // the scalar unit at each call instead of being hoisted out of the chain
+  // loop as 20 loop-invariant SGPRs (which the chain kernels spill to VGPR lanes).
+  k0 = __builtin_amdgcn_readfirstlane(k0);
+  k1 = __builtin_amdgcn_readfirstlane(k1);
+  asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
@@ -107,7 +114,12 @@ __device__ __forceinline__ double uniform(const Stream& s, uint32_t w2, uint32_t
 // not inlined: its log / cos / sqrt temporaries then stay out of the chain
 // loop's register allocation (fewer spills on the hot path; measured -4 % C3
 // together with the momentum cache)
-__device__ __noinline__ double normal(const Stream& s, uint32_t w2, uint32_t w3) {
+#ifndef MDFIT_NORMAL_INLINE
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+double normal(const Stream& s, uint32_t w2, uint32_t w3) {
   const uint4 o = block(s, w2, w3);
   const double u1 = 1.0 - u53(o.x, o.y), u2 = u53(o.z, o.w);
   return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
@@ -1072,6 +1084,688 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PPL == 1 
 }
 
 // ---------------------------------------------------------------------------
+// chain kernel, component-distributed layout (MDFIT_NUTS_CD, the default)
+// ---------------------------------------------------------------------------
+// The slots, tasks, Philox draws and state machine of nuts_chain_kernel, with
+// the chain's 4-vectors (position, momentum, gradient, inverse mass, momentum
+// sums, the trajectory ends and proposals) held one component per lane: lane i
+// of a slot holds component i & 3 (the slot's quads hold copies).  A leapfrog
+// is then 3 instructions instead of 12, a vector costs 2 VGPRs instead of 8, and
+// the hot chain state (dynamics, subtree, tree, step size, counters) lives in
+// registers instead of LDS; the cold vectors (trajectory ends, proposals,
+// Welford) are per-slot LDS arrays of 4.  Dot products (kinetic energy,
+// U-turn criteria) gather the four components and add them in the oracle's
+// order without contraction (oracle/mdfit_nuts.c: kinetic, is_turning).
+#ifndef MDFIT_NUTS_CD
+#define MDFIT_NUTS_CD 1
+#endif
+#ifndef MDFIT_NUTS_CD_WAVES
+#define MDFIT_NUTS_CD_WAVES 4  // 128 VGPRs, no spill with MachineLICM off (build_hip)
+#endif
+
+struct PotC {
+  double U;
+  double g;  // this lane's component of the gradient
+};
+
+// The potential of `potential` / `potential2` with the input and the gradient
+// component-distributed: every lane resolves its own component (c < 3:
+// sigmoid, c == 3: exp), lanes 0-3 of the slot are broadcast.
+template <int PPL>
+__device__ __forceinline__ PotC potential_cd(const PointData pt[PPL], double x, bool whole) {
+  constexpr int kG = PPL == 1 ? 16 : 8;
+  const int c = (int)(threadIdx.x & 3);
+  const bool hi8 = PPL == 2 && (threadIdx.x & 8);
+  const double e = exp(c < 3 ? -fabs(x) : x);
+  const double sp = flog1p(e);
+  const double rr = rcp(1.0 + e);
+  const bool pos = x >= 0.0;
+  const double p = pos ? rr : e * rr, omp = pos ? e * rr : rr;
+  const double lp = pos ? -sp : x - sp, l1p = pos ? -(x + sp) : -sp;
+  const double pr = c == 2 ? lp + 9.0 * l1p : 2.0 * lp + 3.0 * l1p;
+  auto bc = [=](double y, auto n) {
+    constexpr int N = decltype(n)::value;
+    if constexpr (PPL == 1) return rowb<N>(y);
+    else return hi8 ? rowb<8 + N>(y) : rowb<N>(y);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  const double q = bc(p, I0{}), omq = bc(omp, I0{}), prq = bc(pr, I0{});
+  const double A0 = bc(p, I1{}), prA = bc(pr, I1{});
+  const double c0 = bc(p, I2{}), prc = bc(pr, I2{});
+  const double delta = bc(e, I3{}), v3 = bc(x, I3{});
+  const double phi = delta + 2.0;
+  const bool pmd = pt[0].pmd;
+  const double A = pmd ? A0 : 0.0, cc = pmd ? c0 : 0.0;
+  double lprior = prq + v3 - delta * 1e-3;
+  if (pmd) lprior += prA + prc;
+
+  double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  bool bad_lane = pmd && A + cc >= 1.0;
+  double t6l, t6p;
+  LG3 t3b;
+  if constexpr (PPL == 1) {
+    t3b = lg3<false>(pt[0].N + phi);
+    t6l = rowb<15>(t3b.l);  // pad lane: lg(0 + phi)
+    t6p = rowb<15>(t3b.p);
+  } else {
+    t3b = lg3<false>(pt[1].N + phi);
+    const bool src15 = whole || hi8;
+    t6l = src15 ? rowb<15>(t3b.l) : rowb<7>(t3b.l);
+    t6p = src15 ? rowb<15>(t3b.p) : rowb<7>(t3b.p);
+  }
+#pragma unroll
+  for (int pi = 0; pi < PPL; ++pi) {
+    const PointData& pd = pt[pi];
+    double D, dq, dA;
+    if (pmd) {
+      const double w = powk(omq, pd.k);
+      D = fma(A, w, cc);
+      dq = pd.k > 0 ? -A * (double)pd.k * (w * rcp(omq)) : 0.0;
+      dA = w;
+    } else {
+      D = q;
+      dq = 1.0;
+      dA = 0.0;
+    }
+    bad_lane = bad_lane || (pd.valid && !(D < 1.0));
+    const double a = D * phi, b = (1.0 - D) * phi;
+    const LG3 t1 = lg3<false>(pd.y + a);
+    const LG3 t4 = lg3<false>(a);
+    const double la = t1.l - t4.l, Pa = t1.p - t4.p;
+    const LG3 t2 = lg3<false>(pd.N - pd.y + b);
+    const LG3 t5 = lg3<false>(b);
+    const double lb = t2.l - t5.l, Pb = t2.p - t5.p;
+    const LG3 t3 = (PPL == 1 || pi == 1) ? t3b : lg3<false>(pd.N + phi);
+    const double ell = (la + lb) - (t3.l - t6l);
+    const double lD = phi * (Pa - Pb);
+    const double lF = D * Pa + (1.0 - D) * Pb + (t6p - t3.p);
+    if (PPL == 1) {
+      acc[0] = ell;
+      acc[1] = lD * dq;
+      acc[2] = lD * dA;
+      acc[3] = lD;
+      acc[4] = lF;
+    } else if (pd.valid) {
+      acc[0] += ell;
+      acc[1] += lD * dq;
+      acc[2] += lD * dA;
+      acc[3] += lD;
+      acc[4] += lF;
+    }
+  }
+  const int ok = PPL == 1 ? pt[0].valid : 1;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    if constexpr (PPL == 1) {
+      const double s16 = gsum<16>(ok ? acc[j] : 0.0);
+      acc[j] = whole ? s16 + __shfl_xor(s16, 16, 64) : s16;
+    } else {
+      const double s8 = gsum<8>(acc[j]);
+      acc[j] = whole ? s8 + dpp<0x140>(s8) : s8;
+    }
+  }
+  const unsigned long long bm = __ballot(bad_lane);
+  const int sh = (int)(threadIdx.x & (whole ? ~(2 * kG - 1) : ~(kG - 1)));
+  const unsigned long long wm = whole ? (kG == 16 ? 0xFFFFFFFFull : 0xFFFFull) : (kG == 16 ? 0xFFFFull : 0xFFull);
+  const bool bad = ((bm >> sh) & wm) != 0ull;
+  PotC o;
+  o.U = -(acc[0] + lprior);
+  // component c: -(sum * J + prior slope), J = p (1 - p) (c < 3) or delta
+  const double X = c == 0 ? acc[1] : (c == 1 ? acc[2] : (c == 2 ? acc[3] : acc[4]));
+  const double Y = c == 3 ? e : p * omp;
+  const double Z = c == 3 ? 1.0 - e * 1e-3 : (c == 2 ? 1.0 - 10.0 * p : 2.0 - 5.0 * p);
+  o.g = (!pmd && (c == 1 || c == 2)) ? 0.0 : -(X * Y + Z);
+  if (bad || !isfinite(o.U)) {
+    o.U = INFINITY;
+    o.g = 0.0;
+  }
+  return o;
+}
+
+// ((t0 + t1) + t2) + t3 of the slot's four component terms (lanes 0-3 of the
+// slot), the oracle's loop order; the terms of inactive components are 0
+template <int G>
+__device__ __forceinline__ double sum4(double t) {
+  double o[4];
+  slot4<G>(t, o);
+  return ((o[0] + o[1]) + o[2]) + o[3];
+}
+
+// kinetic energy (oracle: kinetic), component-distributed
+template <int G>
+__device__ __forceinline__ double kinetic_cd(bool act, double im, double r) {
+#pragma clang fp contract(off)
+  return 0.5 * sum4<G>(act ? im * r * r : 0.0);
+}
+
+// the U-turn criterion (oracle: is_turning), component-distributed
+template <int G>
+__device__ __forceinline__ bool turning_cd(bool act, double im, double rl, double rr, double rsum) {
+#pragma clang fp contract(off)
+  const double rs = rsum - 0.5 * (rl + rr);
+  const double dl = sum4<G>(act ? im * rl * rs : 0.0);
+  const double dr = sum4<G>(act ? im * rr * rs : 0.0);
+  return dl <= 0.0 || dr <= 0.0;
+}
+
+// the same on full vectors (a checkpoint's criterion on its own lane)
+__device__ __forceinline__ bool turning_full(bool pmd, const double invm[4], const double rl[4], const double rr[4],
+                                             const double rsum[4]) {
+#pragma clang fp contract(off)
+  double dl = 0.0, dr = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!active(pmd, j)) continue;
+    const double rs = rsum[j] - 0.5 * (rl[j] + rr[j]);
+    dl += invm[j] * rl[j] * rs;
+    dr += invm[j] * rr[j] * rs;
+  }
+  return dl <= 0.0 || dr <= 0.0;
+}
+
+// per-slot LDS vectors (component c at [c])
+enum { kVlz, kVlr, kVlg, kVrz, kVrr, kVrg, kVtz, kVtg, kVsz, kVsg, kVwm, kVw2, kVim, kVis, kVtr, kNVec };
+
+// cold per-chain scalars (row-uniform, LDS)
+struct ColdState {
+  Stream st;
+  int64_t taxon;
+  double tpe, spe;  // potential energy of the tree / subtree proposal
+  double eps, t_w, t_acc, u_tr;
+  double x_avg, g_avg, mu;
+  double st_div, st_leap;
+  int sub, attempt, f_call, f_m, f_last, f_dir, t_da, widx, wn, nm_chunk;
+  int t_n, t_depth;
+};
+
+template <int PPL>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUTS_CD_WAVES))) void nuts_chain_cd(
+    const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN, int64_t T, mdfit_opts o,
+    double* __restrict__ out, int* __restrict__ ws, double* __restrict__ samples) {
+  static_assert(PPL == 1 || PPL == 2, "points per lane");
+  constexpr int kG = PPL == 1 ? 16 : 8;  // lanes per chain slot
+  constexpr int kNSlot = kWave / kG;
+  constexpr int kTaskL = 2 * kG;
+  constexpr unsigned long long kTaskMask = kTaskL == 32 ? 0xFFFFFFFFull : 0xFFFFull;
+  constexpr unsigned long long kSlotMask = kG == 16 ? 0xFFFFull : 0xFFull;
+  __shared__ double sv[kNSlot][kNVec][4];
+  __shared__ ColdState scold[kNSlot];
+  __shared__ double sck[8][kWave];                   // checkpoint i of a slot on its lane i: r[4], rsum[4]
+  __shared__ double sck8[PPL == 2 ? kNSlot : 1][8];  // PPL 2: checkpoint 8 of a slot
+  __shared__ double sut[16 * kNSlot], sul[16 * kNSlot], snm[16 * kNSlot];
+  __shared__ int sdb[16 * kNSlot];
+  __shared__ int swin_end[kMaxWin];
+  __shared__ int swin_n;
+  // lane layout (re-derived from an opaque lane index at every trip of the
+  // chain loop: its masks and LDS addresses are recomputed on the fly instead
+  // of being held across the loop, which costs registers)
+#define MDFIT_CD_LAYOUT(LANE)                                                             \
+  const int lane = (LANE);                                                                \
+  const int r = lane & (kTaskL - 1), h = r / kG, i = r & (kG - 1), row = lane / kG;       \
+  const int c = i & 3; /* this lane's vector component */                                 \
+  const int row16 = row * 16;                                                             \
+  const int leader = lane & ~(kTaskL - 1);                                                \
+  double(*V)[4] = sv[row];                                                                \
+  ColdState& C = scold[row];                                                              \
+  (void)h, (void)c, (void)row16, (void)leader, (void)V, (void)C
+  MDFIT_CD_LAYOUT(threadIdx.x);
+  const int qi = blockIdx.x % kQueues;
+  const int64_t tl = T * qi / kQueues, nq = T * (qi + 1) / kQueues - tl;
+  const int W = o.num_warmup, S = o.num_samples;
+
+  // the lane's points: counts kept as integers across the loop (converted at
+  // each evaluation: 2 VGPRs per point instead of 4)
+  struct PointQ {
+    uint32_t y, N;
+    int k, valid;
+  } pq[PPL];
+  int pmdq = 1;
+#pragma unroll
+  for (int p = 0; p < PPL; ++p) {
+    pq[p].valid = PPL == 1 ? i < kNHalf : 0;
+    pq[p].k = PPL == 1 && i < kNHalf ? i : 0;
+    pq[p].y = pq[p].N = 0u;
+  }
+  for (int j = 0; j < 8; ++j) sck[j][lane] = 0.0;
+  if (PPL == 2 && i == 0)
+    for (int j = 0; j < 8; ++j) sck8[row][j] = 0.0;
+  for (int v = 0; v < kNVec; ++v) V[v][c] = (v == kVim || v == kVis) ? 1.0 : 0.0;
+  C.st = make_stream(0, 0, 0);
+  C.taxon = 0;
+  C.tpe = C.spe = C.x_avg = C.g_avg = C.mu = C.st_div = C.st_leap = 0.0;
+  C.eps = 1.0;
+  C.t_w = C.t_acc = C.u_tr = 0.0;
+  C.t_n = C.t_depth = 0;
+  C.sub = C.attempt = C.f_call = C.f_m = C.f_last = C.f_dir = C.t_da = C.widx = C.wn = 0;
+  C.nm_chunk = -1;
+  if (lane < kMaxWin) {
+    int e, n;
+    windows(W, lane, &e, &n);
+    swin_end[lane] = e;
+    if (lane == 0) swin_n = n;
+  }
+  __syncthreads();
+
+  // hot chain state, row-uniform (the vectors: component c)
+  int mode = 0, drained = 0, whole = 0, it = 0;
+  double z = 0.0, rm = 0.0, gr = 0.0, im = 1.0, srs = 0.0;
+  // (the tree's scalars -- weight, acceptance sum, size, depth, merge uniform --
+  // and the step size are touched once per doubling: ColdState)
+  double step = 0.0, e0 = 0.0;
+  double s_w = 0.0, s_acc = 0.0;
+  int leaf_ctr = 0, nleap = 0, s_n = 0, n_leaf = 0, nmax = 1, ul_chunk = -1;
+  int right = 1, t_turn = 0, t_div = 0, s_div = 0;
+
+  while (true) {
+#ifndef MDFIT_CD_HOIST_LAYOUT
+    int lane_o = (int)threadIdx.x;
+    asm volatile("" : "+v"(lane_o));
+    MDFIT_CD_LAYOUT(lane_o);
+#endif
+    // ---- 1. free groups start a task (one atomic per wave-trip) --------------
+    const unsigned long long busy_m = __ballot(mode != 0 && mode != kDone);
+    const bool group_free = ((busy_m >> leader) & kTaskMask) == 0ull;
+    if (group_free) mode = 0;
+    const bool need = group_free && !drained;
+    bool starting = false;
+    if (__any(need)) {
+      const unsigned long long m = __ballot(need && r == 0);
+      int base = 0;
+      if (lane == 0) base = atomicAdd(ws + qi, __popcll(m));
+      base = __shfl(base, 0);
+      if (need) {
+        const int64_t task = (int64_t)base + __popcll(m & ((1ull << leader) - 1ull));
+        if (task >= 4 * nq) {
+          drained = 1;
+          mode = 0;
+        } else {
+          const int kind = (int)(task / nq);
+          C.taxon = tl + task % nq;
+          whole = kind == 0 || kind == 2;
+          C.sub = kind == 0 ? 0 : (kind == 2 ? 1 : (kind == 1 ? 2 : 4) + h);
+          starting = true;
+        }
+      }
+    }
+    if (starting) {
+      const int64_t taxon = C.taxon;
+      const int sub = C.sub;
+      const int pmd_task = sub == 0 || sub == 2 || sub == 3;
+      pmdq = pmd_task;
+#pragma unroll
+      for (int p = 0; p < PPL; ++p) {
+        int colv;
+        if (PPL == 1) {
+          colv = h * kNHalf + pq[p].k;
+        } else if (whole) {
+          pq[p].valid = r < kNHalf;
+          pq[p].k = r < kNHalf ? r : 0;
+          colv = p * kNHalf + pq[p].k;
+        } else {
+          pq[p].valid = 2 * i + p < kNHalf;
+          pq[p].k = pq[p].valid ? 2 * i + p : 0;
+          colv = h * kNHalf + pq[p].k;
+        }
+        pq[p].y = pq[p].valid ? gy[taxon * kLD + colv] : 0u;
+        pq[p].N = pq[p].valid ? gN[taxon * kLD + colv] : 0u;
+      }
+      C.st = make_stream(o.seed, o.index_base + taxon, sub);
+      C.nm_chunk = -1;
+      mode = kInit;
+      C.attempt = 0;
+      it = 0;
+      C.st_div = C.st_leap = 0.0;
+      C.eps = 1.0;
+      step = 0.0;
+      C.f_call = C.f_m = C.f_last = C.f_dir = 0;
+      C.x_avg = C.g_avg = C.mu = 0.0;
+      C.t_da = C.widx = C.wn = 0;
+      const bool act = active(pmd_task, c);
+      z = act ? -2.0 + 4.0 * uniform(C.st, 0xFFFF0000u, (uint32_t)c) : 0.0;
+      rm = gr = 0.0;
+      im = 1.0;
+      V[kVwm][c] = V[kVw2][c] = V[kVtr][c] = 0.0;
+      V[kVim][c] = V[kVis][c] = 1.0;
+    }
+    if (!__any(mode != 0 || !drained)) break;
+    const bool running = mode == kInit || mode == kFind || mode == kIter;
+    if (!__any(running)) continue;
+    const bool pmd = pmdq;
+    const bool act = active(pmd, c);
+    PointData pd[PPL];
+#pragma unroll
+    for (int p = 0; p < PPL; ++p) {
+      pd[p].y = (double)pq[p].y;
+      pd[p].N = (double)pq[p].N;
+      pd[p].k = pq[p].k;
+      pd[p].valid = pq[p].valid;
+      pd[p].pmd = pmdq;
+    }
+
+    // ---- 2. one evaluation: the initial point, or a leapfrog step ------------
+    const double rh = rm - 0.5 * step * gr;
+    const double zev = mode == kInit ? z : z + step * im * rh;
+#ifdef MDFIT_DEV_NOPOT  // development: register demand of the state machine alone
+    PotC P;
+    P.U = zev * zev + pd[0].y;
+    P.g = 2.0 * zev;
+#else
+    const PotC P = potential_cd<PPL>(pd, zev, whole);
+#endif
+    if (!running) continue;
+    const double rn = rh - 0.5 * step * P.g;
+    z = zev;
+
+    bool begin_iter = false, begin_find = false;
+    if (mode == kInit) {
+      if (isfinite(P.U)) {
+        V[kVtz][c] = zev;
+        V[kVtg][c] = P.g;
+        C.tpe = P.U;
+        C.eps = 1.0;
+        C.f_call = 0;
+        begin_find = true;
+      } else if (++C.attempt >= 100) {
+        // no finite initial point: NaN draws, status 2
+        const int64_t taxon = C.taxon;
+        const int sub = C.sub;
+        for (int s = i; s < S; s += kG)
+          if (!whole || h == 0)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              samples[((taxon * MDFIT_NSUBFIT + sub) * (int64_t)S + s) * 4 + j] = NAN;
+        if ((!whole || h == 0) && i < 4) {
+          double* dg = out + taxon * MDFIT_NOUT + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * sub;
+          dg[4 + i] = i == 2 ? (double)MDFIT_NONFINITE : NAN;
+        }
+        mode = kDone;
+      } else {
+        z = act ? -2.0 + 4.0 * uniform(C.st, 0xFFFF0000u + (uint32_t)C.attempt, (uint32_t)c) : 0.0;
+      }
+    } else if (mode == kFind) {
+      const double de = (P.U + kinetic_cd<kG>(act, im, rn)) - e0;
+      const int dnew = log(kTarget) < -de ? 1 : -1;
+      const int f_last = C.f_dir;
+      C.f_last = f_last;
+      C.f_dir = dnew;
+      const int f_m = ++C.f_m;
+      const bool cont = (C.eps > kTiny || dnew >= 0) && (C.eps < kHuge || dnew <= 0) && (f_last == 0 || dnew == f_last) &&
+                        f_m < 4000;
+      if (cont) {
+        begin_find = true;
+      } else {
+        C.mu = log(10.0 * C.eps);
+        C.x_avg = C.g_avg = 0.0;
+        C.t_da = 0;
+        begin_iter = true;
+      }
+    } else {  // kIter: a leaf of the subtree
+      ++nleap;
+      double rn4[4], im4[4];
+      slot4<kG>(rn, rn4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) im4[j] = V[kVim][j];
+      double de;
+      {
+#pragma clang fp contract(off)
+        double k = 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (active(pmd, j)) k += im4[j] * rn4[j] * rn4[j];
+        de = (P.U + 0.5 * k) - e0;
+      }
+      if (isnan(de)) de = INFINITY;
+      const double w = -de;
+      const int dv = de > kMaxDelta;
+      const double acc = de > 0.0 ? exp(-de) : 1.0;
+      if (n_leaf == 0) {
+        V[kVsz][c] = zev;
+        V[kVsg][c] = P.g;
+        C.spe = P.U;
+        srs = rn;
+        s_w = w;
+        s_acc = acc;
+        s_n = 1;
+      } else {
+        const double m = fmax(s_w, w);
+        const double e = exp(-fabs(s_w - w));
+        const double nw = m == -INFINITY ? -INFINITY : m + flog1p(e);
+        const double prob = (w >= s_w ? 1.0 : e) * rcp(1.0 + e);
+        if ((leaf_ctr >> 4) != ul_chunk) {  // next 16 leaf uniforms, 16 / kG per lane
+#pragma unroll
+          for (int e2 = 0; e2 < 16 / kG; ++e2) {
+            const int ix = i + kG * e2;
+            sul[row16 + ix] = uniform(C.st, (uint32_t)it, 32u + (uint32_t)(leaf_ctr & ~15) + (uint32_t)ix);
+          }
+          ul_chunk = leaf_ctr >> 4;
+        }
+        if (sul[row16 + (leaf_ctr & 15)] < prob) {
+          V[kVsz][c] = zev;
+          V[kVsg][c] = P.g;
+          C.spe = P.U;
+        }
+        s_w = nw;
+        srs += rn;
+        s_acc += acc;
+        s_n += 1;
+      }
+      s_div = dv;
+      ++leaf_ctr;
+      int imin, imax;
+      ckpt_idxs(n_leaf, &imin, &imax);
+      double srs4[4];
+      slot4<kG>(srs, srs4);
+      if ((n_leaf & 1) == 0 && i == imax) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          sck[j][lane] = rn4[j];
+          sck[4 + j][lane] = srs4[j];
+        }
+      }
+      if (PPL == 2 && (n_leaf & 1) == 0 && imax == 8 && i == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          sck8[row][j] = rn4[j];
+          sck8[row][4 + j] = srs4[j];
+        }
+      }
+      bool my_turn = false;
+      if (i >= imin && i <= imax) {
+#pragma clang fp contract(off)
+        double ck_r[4], sub_rsum[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          ck_r[j] = sck[j][lane];
+          sub_rsum[j] = srs4[j] - sck[4 + j][lane] + ck_r[j];
+        }
+        my_turn = turning_full(pmd, im4, ck_r, rn4, sub_rsum);
+      }
+      if (PPL == 2 && i == 0 && imin <= 8 && imax >= 8) {
+#pragma clang fp contract(off)
+        double ck_r[4], sub_rsum[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          ck_r[j] = sck8[row][j];
+          sub_rsum[j] = srs4[j] - sck8[row][4 + j] + ck_r[j];
+        }
+        my_turn = my_turn || turning_full(pmd, im4, ck_r, rn4, sub_rsum);
+      }
+      const unsigned long long tm = __ballot(my_turn);
+      const int s_turn = ((tm >> (lane & ~(kG - 1))) & kSlotMask) != 0ull;
+      ++n_leaf;
+      rm = rn;
+      gr = P.g;
+      if (s_turn || s_div || n_leaf == nmax) {
+        // merge the subtree into the tree: biased progressive sampling
+        const double em = exp(-fabs(C.t_w - s_w));
+        const double prob = (s_turn || s_div) ? 0.0 : (s_w > C.t_w ? 1.0 : em);
+        if (C.u_tr < prob) {
+          V[kVtz][c] = V[kVsz][c];
+          V[kVtg][c] = V[kVsg][c];
+          C.tpe = C.spe;
+        }
+        const double olr = right ? V[kVlr][c] : V[kVrr][c];  // r of the untouched end
+        if (right) {
+          V[kVrz][c] = z;
+          V[kVrr][c] = rm;
+          V[kVrg][c] = gr;
+        } else {
+          V[kVlz][c] = z;
+          V[kVlr][c] = rm;
+          V[kVlg][c] = gr;
+        }
+        {
+          const double m = fmax(C.t_w, s_w);
+          C.t_w = m == -INFINITY ? -INFINITY : m + flog1p(em);
+        }
+        const double trs = V[kVtr][c] + srs;
+        V[kVtr][c] = trs;
+        t_turn = s_turn || (right ? turning_cd<kG>(act, im, olr, rm, trs) : turning_cd<kG>(act, im, rm, olr, trs));
+        t_div = s_div;
+        C.t_acc += s_acc;
+        C.t_n += s_n;
+        ++C.t_depth;
+        if (C.t_depth >= kMaxDepth || t_turn || t_div) {
+          // ---- the transition is complete: adapt or keep the draw ----------
+          const double accp = C.t_acc / (double)C.t_n;
+          if (it < W) {
+            const int t_da = ++C.t_da;
+            const double gg = kTarget - accp;
+            const double inv = 1.0 / (t_da + 10.0);
+            const double g_avg = (1.0 - inv) * C.g_avg + gg * inv;
+            C.g_avg = g_avg;
+            const double x_t = C.mu - sqrt((double)t_da) * 20.0 * g_avg;  // / gamma (0.05)
+            const double sq = sqrt((double)t_da);
+            const double wt = 1.0 / (sq * sqrt(sq));  // t^-0.75
+            const double x_avg = (1.0 - wt) * C.x_avg + wt * x_t;
+            C.x_avg = x_avg;
+            C.eps = exp(it == W - 1 ? x_avg : x_t);
+            if (C.eps < kTiny) C.eps = kTiny;
+            const int widx = C.widx;
+            const int wend = widx < kMaxWin ? swin_end[widx] : -1, nwin = swin_n;
+            const bool middle = widx > 0 && widx < nwin - 1;
+            if (middle) {
+              const int wn = ++C.wn;
+              if (act) {
+                const double tz = V[kVtz][c], wmean = V[kVwm][c];
+                const double d0 = tz - wmean;
+                const double wm1 = wmean + d0 / wn;
+                V[kVwm][c] = wm1;
+                V[kVw2][c] = V[kVw2][c] + d0 * (tz - wm1);
+              }
+            }
+            const bool at_end = it == wend;
+            if (at_end && middle) {
+              const int wn = C.wn;
+              if (act) {
+                const double var = V[kVw2][c] / (wn - 1);
+                im = ((double)wn / (wn + 5.0)) * var + 1e-3 * (5.0 / (wn + 5.0));
+                V[kVis][c] = sqrt(1.0 / im);
+                V[kVim][c] = im;
+                V[kVwm][c] = V[kVw2][c] = 0.0;
+              }
+              C.wn = 0;
+              ++C.f_call;
+              begin_find = true;
+            }
+            if (at_end) C.widx = widx + 1;
+          } else {
+            const int64_t sidx = ((C.taxon * MDFIT_NSUBFIT + C.sub) * (int64_t)S + (it - W)) * 4;
+            if ((!whole || h == 0) && i < 4) {
+              const double zj = V[kVtz][c];
+              samples[sidx + i] = i == 3 ? exp(zj) + 2.0 : ((i == 0 || pmd) ? 1.0 / (1.0 + exp(-zj)) : 0.0);
+            }
+            C.st_div += t_div ? 1.0 : 0.0;
+            C.st_leap += (double)nleap;
+          }
+          ++it;
+          if (it == W + S) {
+            if ((!whole || h == 0) && i < 4) {
+              double* dg = out + C.taxon * MDFIT_NOUT + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * C.sub;
+              dg[4 + i] = i == 0 ? C.eps : (i == 1 ? C.st_leap / S : (i == 2 ? (double)MDFIT_OK : C.st_div));
+            }
+            mode = kDone;
+          } else if (!begin_find) {
+            begin_iter = true;
+          }
+        } else {
+          // next doubling
+          const int j = C.t_depth;
+          right = sdb[row16 + j] != 0;
+          C.u_tr = sut[row16 + j];
+          n_leaf = 0;
+          nmax = 1 << j;
+          step = right ? C.eps : -C.eps;
+          z = right ? V[kVrz][c] : V[kVlz][c];
+          rm = right ? V[kVrr][c] : V[kVlr][c];
+          gr = right ? V[kVrg][c] : V[kVlg][c];
+        }
+      }  // (else: the next leaf of the subtree continues from (z, r, g) with the same step)
+    }
+
+    if (begin_find) {
+      // one probe of find_reasonable_step_size from the current state
+      if (mode != kFind || C.f_m == 0) {
+        C.f_m = 0;
+        C.f_last = C.f_dir = 0;
+      }
+      mode = kFind;
+      C.eps = ldexp(C.eps, C.f_dir);
+      const double nj = normal(C.st, 0xFFFE0000u + 4096u * (uint32_t)C.f_call + (uint32_t)C.f_m, (uint32_t)c);
+      rm = act ? nj * V[kVis][c] : 0.0;
+      z = V[kVtz][c];
+      gr = V[kVtg][c];
+      e0 = C.tpe + kinetic_cd<kG>(act, im, rm);
+      step = C.eps;
+    }
+    if (begin_iter) {
+      mode = kIter;
+      // this iteration's momenta from the 4-iteration cache
+      if ((it >> 2) != C.nm_chunk) {
+#pragma unroll
+        for (int e2 = 0; e2 < 16 / kG; ++e2) {
+          const int ix = i + kG * e2;
+          snm[row16 + ix] = normal(C.st, (uint32_t)((it & ~3) + (ix >> 2)), (uint32_t)(ix & 3));
+        }
+        C.nm_chunk = it >> 2;
+      }
+      const double nj = snm[row16 + 4 * (it & 3) + c];
+      rm = act ? nj * V[kVis][c] : 0.0;
+      z = V[kVtz][c];
+      gr = V[kVtg][c];
+      V[kVlz][c] = V[kVrz][c] = z;
+      V[kVlr][c] = V[kVrr][c] = rm;
+      V[kVlg][c] = V[kVrg][c] = gr;
+      V[kVtr][c] = rm;
+      e0 = C.tpe + kinetic_cd<kG>(act, im, rm);
+      C.t_w = 0.0;
+      C.t_acc = 0.0;
+      C.t_n = 0;
+      C.t_depth = 0;
+      t_turn = t_div = 0;
+      leaf_ctr = 0;
+      nleap = 0;
+      // this iteration's doubling draws, lane j of the slot for depth j
+#pragma unroll
+      for (int e2 = 0; e2 < 16 / kG; ++e2) {
+        const int ix = i + kG * e2;
+        sdb[row16 + ix] = (int)(block(C.st, (uint32_t)it, 4u + 2u * (uint32_t)ix).x & 1u);
+        sut[row16 + ix] = uniform(C.st, (uint32_t)it, 5u + 2u * (uint32_t)ix);
+      }
+      ul_chunk = -1;
+      right = sdb[row16] != 0;
+      C.u_tr = sut[row16];
+      n_leaf = 0;
+      nmax = 1;
+      step = right ? C.eps : -C.eps;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // post kernel: one wave per taxon
 // ---------------------------------------------------------------------------
 // frac = obs / N of one predictive Beta-Binomial draw (oracle: predictive_frac)
@@ -1415,6 +2109,27 @@ __global__ __launch_bounds__(kWave) void nuts_potential_kernel(const int32_t* __
 #pragma unroll
   for (int j = 0; j < 4; ++j) v[j] = gv[it * 4 + j];
   Pot P;
+  if (MDFIT_NUTS_CD) {  // the component-distributed potential of nuts_chain_cd
+    constexpr int kP = MDFIT_NUTS_PPL;
+    PointData pd[kP];
+#pragma unroll
+    for (int p = 0; p < kP; ++p) {
+      const int k = kP == 1 ? (lane & 15) : (whole ? (lane & 15) : 2 * (lane & 7) + p);
+      const int hh = kP == 1 ? ((lane & 31) >> 4) : p;
+      pd[p].pmd = model[it] == 0;
+      pd[p].valid = (kP == 1 ? (whole ? lane < 32 : lane < 16) : (whole ? lane < 16 : lane < 8)) && k < kNHalf;
+      pd[p].k = pd[p].valid ? k : 0;
+      const int col = pd[p].valid ? (whole ? hh : dir) * kNHalf + k : 0;
+      pd[p].y = pd[p].valid ? (double)gy[it * kLD + col] : 0.0;
+      pd[p].N = pd[p].valid ? (double)gN[it * kLD + col] : 0.0;
+    }
+    const PotC pc = potential_cd<kP>(pd, v[lane & 3], whole);
+    if (lane < 4) {
+      if (lane == 0) U[it] = pc.U;
+      g[it * 4 + lane] = pc.g;
+    }
+    return;
+  }
   if (MDFIT_NUTS_PPL == 1) {
     const int r = lane & 31, h = r >> 4, k = r & 15;
     PointData pd;
@@ -1474,11 +2189,10 @@ int fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t 
   // (MDFIT_DEV_PER_CU: waves per CU forced, development A/B; the chain
   // kernel's waves never wait on each other, so any grid drains)
   const char* force = std::getenv("MDFIT_DEV_PER_CU");
-  const int64_t g =
-      host::fit_grid(nuts_chain_kernel<kPPL>, 4 * n_taxa, kPPL == 1 ? 2 : 4, 0, force ? std::atoi(force) : 0);
+  auto chain = MDFIT_NUTS_CD ? nuts_chain_cd<kPPL> : nuts_chain_kernel<kPPL>;
+  const int64_t g = host::fit_grid(chain, 4 * n_taxa, kPPL == 1 ? 2 : 4, 0, force ? std::atoi(force) : 0);
   host::prof_mark(1, s);
-  hipLaunchKernelGGL(nuts_chain_kernel<kPPL>, dim3((unsigned)g), dim3(kWave), 0, s, y, N, n_taxa, o, out, ws,
-                     samples);
+  hipLaunchKernelGGL(chain, dim3((unsigned)g), dim3(kWave), 0, s, y, N, n_taxa, o, out, ws, samples);
   if (int rc = host::check_launch("nuts_chain_kernel")) return rc;
   host::prof_mark(2, s);
   size_t sv_bytes = sizeof(double);
