@@ -1452,6 +1452,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
     PotC P;
     P.U = zev * zev + pd[0].y;
     P.g = 2.0 * zev;
+#elif defined(MDFIT_NUTS_POT_TWICE)  // development: marginal cost of one potential evaluation
+    const PotC P0 = potential_cd<PPL>(pd, zev * (1.0 + 1e-300 * (double)it), whole);
+    PotC P = potential_cd<PPL>(pd, zev, whole);
+    P.U += 0.0 * P0.U * (double)(it > (1 << 30));
 #else
     const PotC P = potential_cd<PPL>(pd, zev, whole);
 #endif
