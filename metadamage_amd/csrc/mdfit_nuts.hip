@@ -1976,7 +1976,11 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
   }
 
   // ---- waic_i per chain and point (fits.py:126-172), lanes over draws ----------
+#ifdef MDFIT_DEV_POST_NOWAIC  // development: timing split of the post kernel
+  for (int s = 0; s < 0; ++s) {
+#else
   for (int s = 0; s < MDFIT_NSUBFIT; ++s) {
+#endif
     const bool pmd = s == 0 || s == 2 || s == 3;
     const int lo = (s == 3 || s == 5) ? kNHalf : 0, hi = s < 2 ? kNPos : lo + kNHalf;
     for (int col = lo; col < hi; ++col) {
@@ -2070,9 +2074,15 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
       m3[0] = m3[1] = m3[2] = NAN;
     } else {
       const Stream st = make_stream(o.seed, o.index_base + t, s);
+#ifdef MDFIT_DEV_POST_NODRAW
+      for (int x = lane; x < S; x += kWave) s_v[x] = smp[((int64_t)s * S + x) * 4] * (double)(col + 1);
+#else
       for (int x = lane; x < S; x += kWave) s_v[x] = predictive_frac(st, x, col, k, nn, smp + ((int64_t)s * S + x) * 4);
+#endif
       __syncthreads();
+#ifndef MDFIT_DEV_POST_NOSORT
       lds_sort(s_v, S);
+#endif
       median_hpdi(s_v, S, m3);
       __syncthreads();
     }
