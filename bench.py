@@ -470,11 +470,11 @@ def nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, 
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": pmc_traffic("nuts_chain_kernel", T),
-            "kernel": "nuts_chain_kernel",
+            "traffic": pmc_traffic("nuts_chain_cd", T),
+            "kernel": "nuts_chain_cd",
             "note": "algorithmic bytes per SURVEY.md 8(d) (y,N in + 26 result fields + 90 prediction values out "
             "= 808 B/taxon); the HBM fraction is structural (~2e6 leapfrog point evaluations per taxon): the kernel "
-            "is FP64-VALU bound (DESIGN.md 9); traffic is the PMC-measured HBM bytes, dominated by the draws",
+            "is FP64-VALU / latency bound (DESIGN.md 9); traffic is the PMC-measured HBM bytes, dominated by the draws",
             "kernel_ms_avg": round(k_avg_s * 1e3, 3),
             "bytes_per_taxon": bytes_per_taxon,
             "hbm_intermediate": {

@@ -74,7 +74,7 @@ def main() -> None:
     if nuts and nf and nw:
         shutil.copy(nf[0], prof / f"{tag}_nuts_pmc_fetch_size.csv")
         shutil.copy(nw[0], prof / f"{tag}_nuts_pmc_write_size.csv")
-        write_summary(prof, tag, "nuts_chain_kernel", NUTS_TAXA, NUTS_BYTES_PER_TAXON, 808,
+        write_summary(prof, tag, "nuts_chain_cd", NUTS_TAXA, NUTS_BYTES_PER_TAXON, 808,
                       prof / f"{tag}_nuts_kernel_stats.csv", prof / f"{tag}_nuts_pmc_fetch_size.csv",
                       prof / f"{tag}_nuts_pmc_write_size.csv", "python bench.py --mode nuts")
 
