@@ -1358,6 +1358,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   double s_w = 0.0, s_acc = 0.0;
   int leaf_ctr = 0, nleap = 0, s_n = 0, n_leaf = 0, nmax = 1, ul_chunk = -1;
   int right = 1, t_turn = 0, t_div = 0, s_div = 0;
+#ifdef MDFIT_DEV_UTIL
+  unsigned long long util_trips = 0, util_busy = 0;
+#endif
 
   while (true) {
 #ifndef MDFIT_CD_HOIST_LAYOUT
@@ -1433,6 +1436,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
     if (!__any(mode != 0 || !drained)) break;
     const bool running = mode == kInit || mode == kFind || mode == kIter;
     if (!__any(running)) continue;
+#ifdef MDFIT_DEV_UTIL  // development: slot utilisation (trips with a running slot / all slot-trips)
+    {
+      const unsigned long long rb = __ballot(running && i == 0);
+      util_trips += 1;
+      util_busy += __popcll(rb);
+    }
+#endif
     const bool pmd = pmdq;
     const bool act = active(pmd, c);
     PointData pd[PPL];
@@ -1767,6 +1777,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       step = right ? C.eps : -C.eps;
     }
   }
+#ifdef MDFIT_DEV_UTIL
+  if (threadIdx.x == 0) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(ws + 32), util_trips);
+    atomicAdd(reinterpret_cast<unsigned long long*>(ws + 34), util_busy);
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------
