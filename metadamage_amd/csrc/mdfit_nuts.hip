@@ -1708,6 +1708,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         } else {
           // next doubling
           const int j = C.t_depth;
+          if (j == 8) {  // the draws of depths 8 and 9 (entries 8, 9 of the caches)
+            if (i < 4) {
+              const int jj = 8 + (i & 1);
+              const uint4 b = block(C.st, (uint32_t)it, (i < 2 ? 4u : 5u) + 2u * (uint32_t)jj);
+              if (i < 2) sdb[row16 + jj] = (int)(b.x & 1u);
+              else sut[row16 + jj] = u53(b.x, b.y);
+            }
+          }
           right = sdb[row16 + j] != 0;
           C.u_tr = sut[row16 + j];
           n_leaf = 0;
@@ -1762,12 +1770,15 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       t_turn = t_div = 0;
       leaf_ctr = 0;
       nleap = 0;
-      // this iteration's doubling draws, lane j of the slot for depth j
+      // this iteration's doubling draws for depths 0-7, one Philox block per
+      // entry: entry e < 8 the direction bit of depth e, entry 8 + e its merge
+      // uniform (depths 8-9, reached by a few iterations, at that doubling)
 #pragma unroll
       for (int e2 = 0; e2 < 16 / kG; ++e2) {
-        const int ix = i + kG * e2;
-        sdb[row16 + ix] = (int)(block(C.st, (uint32_t)it, 4u + 2u * (uint32_t)ix).x & 1u);
-        sut[row16 + ix] = uniform(C.st, (uint32_t)it, 5u + 2u * (uint32_t)ix);
+        const int ix = i + kG * e2, j = ix & 7;
+        const uint4 b = block(C.st, (uint32_t)it, (ix < 8 ? 4u : 5u) + 2u * (uint32_t)j);
+        if (ix < 8) sdb[row16 + j] = (int)(b.x & 1u);
+        else sut[row16 + j] = u53(b.x, b.y);
       }
       ul_chunk = -1;
       right = sdb[row16] != 0;
