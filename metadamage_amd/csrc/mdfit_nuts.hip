@@ -1363,6 +1363,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
 #endif
 
   while (true) {
+    // (-DMDFIT_CD_HOIST_LAYOUT, development: the layout of the prologue held
+    // across the loop instead -- 33 VGPRs spilled at 4 waves/SIMD)
 #ifndef MDFIT_CD_HOIST_LAYOUT
     int lane_o = (int)threadIdx.x;
     asm volatile("" : "+v"(lane_o));
