@@ -52,7 +52,6 @@ sys.path.insert(0, str(ROOT))
 TAXA_PER_GPU = 10_000
 C4_TAXA = 1_000_000
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-NODE_GPUS = 8  # one MI355X node
 # bytes per taxon:
 #  algorithmic: y,N 2x30x4 in + 26 numeric result fields x8 out
 #  fit_kernel as built: y,N 2x30x4 + 6 initial points 6x4x8 in, 6 sub-fit records 6x8x8 out
@@ -569,24 +568,59 @@ def cpu_baseline_nuts(b, threads: int):  # threads: the core share (host_cores)
     t0 = time.perf_counter()
     ref = lib.nuts_batch(b.y[:n], b.N[:n], b.mm[:n], threads=nthr, keep_samples=True)
     dt = time.perf_counter() - t0
-    n1 = 4
+    n1 = 32  # the thread scaling on one fixed sample: its first 32 taxa on 1 and on nthr threads
     t1 = time.perf_counter()
     lib.nuts_batch(b.y[:n1], b.N[:n1], b.mm[:n1], threads=1)
     d1 = time.perf_counter() - t1
+    t2 = time.perf_counter()
+    lib.nuts_batch(b.y[:n1], b.N[:n1], b.mm[:n1], threads=nthr)
+    d2 = time.perf_counter() - t2
     return {
         "value": round(n / dt, 2),
         "unit": "fits/s",
         "cores": nthr,
         "kind": "port",
-        "sample": f"first {n} taxa of the rank-0 workload on {nthr} OpenMP threads ({dt:.2f} s); "
-        f"1-thread rate on the first {n1}: {n1 / d1:.2f} fits/s",
+        "sample": f"first {n} taxa of the rank-0 workload on {nthr} OpenMP threads ({dt:.2f} s)",
+        "thread_curve": {"taxa": n1, "fits_per_s": {"1": round(n1 / d1, 2), str(nthr): round(n1 / d2, 2)},
+                         "efficiency": round(d1 / d2 / nthr, 3)},
         "single_thread_value": round(n1 / d1, 2),
+        "host": cpu_host(),
     }, ref
+
+
+def cpu_host() -> dict:
+    """What the CPU baseline runs on: the affinity set, the cgroup CPU quota
+    (v2 cpu.max, v1 cfs quota / period), and the physical cores behind the
+    affinity set (SMT siblings share one)."""
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            txt = Path(path).read_text().split()
+        except OSError:
+            continue
+        if path.endswith("cpu.max") and txt and txt[0] != "max":
+            quota = round(int(txt[0]) / int(txt[1]), 2)
+        elif path.endswith("quota_us") and txt and int(txt[0]) > 0:
+            per = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+            quota = round(int(txt[0]) / per, 2)
+        break
+    cores = set()
+    for c in aff:
+        try:
+            t = Path(f"/sys/devices/system/cpu/cpu{c}/topology")
+            cores.add(((t / "physical_package_id").read_text().strip(), (t / "core_id").read_text().strip()))
+        except OSError:
+            cores.add(("?", str(c)))
+    return {"affinity_cpus": len(aff), "cgroup_cpu_quota": quota, "physical_cores_in_affinity": len(cores),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "cpus_in_host": os.cpu_count()}
 
 
 def cpu_baseline(b, cores: int, visible: int):
     """The CPU oracle (oracle/libmdfit_oracle.c, C + OpenMP, same algorithm)
-    on the whole workload, timed on this host's core share: median of 5."""
+    on the whole workload, timed on this host's core share: median of 5; plus
+    the thread-scaling curve on one fixed sample (the same taxa at every
+    thread count)."""
     from oracle.oracle import OracleLib
 
     lib = OracleLib()
@@ -597,10 +631,18 @@ def cpu_baseline(b, cores: int, visible: int):
         ref = lib.fit_batch(b.y, b.N, b.mm, threads=cores)
         times.append(time.perf_counter() - t0)
     dt = float(np.median(times))
-    n1 = 300
-    t1 = time.perf_counter()
-    lib.fit_batch(b.y[:n1], b.N[:n1], b.mm[:n1], threads=1)
-    d1 = time.perf_counter() - t1
+    n_curve = min(b.n_taxa, 2000)
+    curve = {}
+    for th in sorted({1, 2, 4, 8, 16, cores}):
+        if th > cores:
+            continue
+        ts = []
+        for _ in range(3 if th > 1 else 1):
+            t1 = time.perf_counter()
+            lib.fit_batch(b.y[:n_curve], b.N[:n_curve], b.mm[:n_curve], threads=th)
+            ts.append(time.perf_counter() - t1)
+        curve[str(th)] = round(n_curve / float(np.median(ts)), 1)
+    one = curve["1"]
     return {
         "value": round(b.n_taxa / dt, 1),
         "unit": "fits/s",
@@ -608,21 +650,17 @@ def cpu_baseline(b, cores: int, visible: int):
         "host_cpus_visible": visible,
         "kind": "port",
         "sample": f"all {b.n_taxa} taxa of the rank-0 workload on {cores} OpenMP threads, median of 5 runs "
-        f"({dt:.2f} s; min {min(times):.2f}, max {max(times):.2f}); 1-thread rate on the first {n1}: "
-        f"{n1 / d1:.1f} fits/s",
-        "single_thread_value": round(n1 / d1, 1),
-        "node_estimate": {
-            "value": round(b.n_taxa / dt * NODE_GPUS * 16 / cores, 1),
-            "cores": NODE_GPUS * 16,
-            "kind": "extrapolated",
-            "note": f"the node's CPU share beside an {NODE_GPUS}-GPU line ({NODE_GPUS} x the 16-thread share per "
-            "GPU), scaled linearly from the measured rate on this rank's share (the taxa are independent, the "
-            f"measured {cores}-thread parallel efficiency vs 1 thread is "
-            f"{b.n_taxa / dt / (cores * n1 / d1):.2f}); not run at that width: a one-GPU box grants "
-            "16 threads of its host (OMP_NUM_THREADS), running the oracle on all visible CPUs would take "
-            "other jobs' cores",
+        f"({dt:.3f} s; min {min(times):.3f}, max {max(times):.3f})",
+        "thread_curve": {
+            "taxa": n_curve,
+            "fits_per_s": curve,
+            "efficiency": {k: round(v / (int(k) * one), 3) for k, v in curve.items()},
+            "note": f"the first {n_curve} taxa at every thread count (1 thread: one run, others median of 3)",
         },
-        "note": "cores = the process's CPU share (affinity / OMP_NUM_THREADS: 16 per GPU on the box)",
+        "host": cpu_host(),
+        "note": "cores = the process's CPU share (affinity / OMP_NUM_THREADS: 16 per GPU on the box); the "
+        "oracle evaluates lnGamma with the reentrant lgamma_r (plain lgamma's global signgam made 16 threads "
+        "fight over one cache line: 1.8x one thread until round 3)",
     }, ref
 
 

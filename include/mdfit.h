@@ -138,17 +138,21 @@ void mdfit_default_opts(mdfit_opts* opts);
  *   workspace : device buffer of mdfit_workspace_bytes(n_taxa) bytes (work
  *               queues, the PMD-all mode for the HPDI, the wide-window list:
  *               MAP 256 B + 48 B per taxon below 60k taxa, + 4,800 B more
- *               per taxon from 60k)
+ *               per taxon from 60k, + the HPDI stream's defer list:
+ *               min(120 B per taxon, 512 KB))
  *   hip_stream: hipStream_t or NULL.  MAP: the record assembly runs on a
  *               library-owned side stream (one per device, created once),
  *               forked from and joined back into hip_stream by events on every
  *               return path, so the call stays ordered on hip_stream and
  *               capturable in a graph.  MAP below 60k taxa: the predictive
  *               HPDI kernel runs beside the fit kernel and waits for modes
- *               the fit kernel's waves publish; the two grids are sized to be
- *               co-resident on an otherwise idle device.  Run calls on one
- *               device one after another (one stream, or ordered streams),
- *               not concurrently with other long-running kernels.
+ *               the fit kernel's waves publish (release / acquire); the two
+ *               grids are sized to be co-resident on an otherwise idle device.
+ *               The waits are bounded: a wave that makes no progress for 1 ms
+ *               hands its items to the HPDI launch after the fit and exits, so
+ *               concurrent calls or other kernels on the device (e.g. an RCCL
+ *               collective) cost time, never a hang.  Fastest when calls on
+ *               one device run one after another.
  *   n_taxa    : at most 2^25 per call (MAP: int32 position indices)
  * Replaces compute_fits' per-taxon loop (fits.py:477-526, 569-626, 709-730).
  */

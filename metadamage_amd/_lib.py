@@ -91,6 +91,10 @@ class MdfitOpts(ctypes.Structure):
 
 
 MODE_MAP, MODE_NUTS = 0, 1
+# MAP: below this many taxa per call the predictive HPDI streams beside the fit
+# kernel; from it the workspace also holds the wide-window records
+# (kStreamMaxTaxa, csrc/mdfit.hip)
+STREAM_MAX_TAXA = 60_000
 SAMPLES_OFFSET = 256  # NUTS workspace: double[T][6][S][4] draws after the queue counters
 
 

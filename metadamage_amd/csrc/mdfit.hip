@@ -76,15 +76,33 @@ __device__ __forceinline__ unsigned long long stamp() {
 //   [9]    hpdi_stream_kernel's item claim counter
 //   [10]   "fit_kernel has started" (hpdi_stream_kernel waits on the list only then)
 //   [16, 19) the wide-window list counters of K4a/K4b (the array entry point)
-// then the ready list: double[T][kReadyStride] = (q, A, c, phi, taxon, tag),
-// zeroed by K0 every call (so no entry of an earlier call or of whatever the
-// buffer held before can pass for a published one: a tag is only ever
-// kReadyTag once this call's fit kernel has written that entry)
+// then the ready list: uint64[T][kReadyStride] = ~bits of (q, A, c, phi,
+// taxon), a spare word; zeroed by K0 every call (so no entry of an earlier
+// call or of whatever the buffer held before can pass for a published one: a
+// field is non-zero only once this call's fit kernel has written it)
 //   [11]   corrupt ready entries met by hpdi_stream_kernel (0; a diagnostic)
+//   [32, 36) the defer list's counters (see hpdi_stream_kernel); the list
+//          itself (int32 items, kDeferCap at most) ends the workspace
 constexpr int kWsReady = 8, kWsClaim = 9, kWsStarted = 10, kWsBad = 11;
+// the HPDI stream's defer list (hpdi_stream_kernel), on a 128-B line of their
+// own (away from the counters the fit kernel's atomics hit): [32] reservations
+// (+ kDefClosed once the late launch has closed it), [33] slots written, [34]
+// the late launch's claim counter over them, [35] an early wave has deferred
+// (the others stop too)
+constexpr int kWsDefRes = 32, kWsDefDone = 33, kWsDefClaim = 34, kWsEarlyQuit = 35;
+constexpr unsigned kDefClosed = 0x40000000u;
 constexpr int kReadyStride = 6;
 static_assert(kReadyStride == MDFIT_NSUBFIT, "K0 zeroes the ready list with one thread per (taxon, sub-fit)");
-constexpr uint64_t kReadyTag = 0x4D44464954524459ull;  // "MDFITRDY"
+// a ready-list field holds the bit complement of its value: zero = not yet
+// written this call (a double's complement is zero only for the all-ones NaN
+// pattern, which ready_put canonicalises away; a taxon index's only for -1)
+__device__ __forceinline__ void ready_put(uint64_t* f, double v) {
+  __hip_atomic_store(f, ~(uint64_t)__double_as_longlong(isnan(v) ? NAN : v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ready_get(const uint64_t* f) {
+  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 constexpr int kHpdiCtr = 16;  // workspace ints: [16] front-list count, [17] claim counter, [18] back-list count
 
 // ---------------------------------------------------------------------------
@@ -659,9 +677,14 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
           // the PMD-all fit just ended: publish its (q, A, c, phi) -- make_theta's
           // arithmetic, NaN for invalid input -- as the next entry of the ready
           // list that hpdi_stream_kernel consumes beside this kernel (the
-          // predictive HPDI, MDFIT-HPDI v1).  Six 8-byte agent-scope (sc1)
-          // stores by lanes 0..5 of the slot, the tag last, behind the
-          // wave's store wait: a reader that sees the tag sees the entry.
+          // predictive HPDI, MDFIT-HPDI v1).  The slot's first lane writes the
+          // entry's five fields as relaxed agent-scope atomic stores of their
+          // bit complements (ready_put): K0 zeroed the list, so a field reads
+          // non-zero exactly once this call has written it, and a reader takes
+          // the entry when all five do -- no cross-field ordering is needed,
+          // hence no fence (an agent-scope release / acquire pair costs an L2
+          // write-back per publication and an L2 invalidate per take on this
+          // multi-XCD part: C2 1.24 -> 1.45 ms, measured)
           auto sig = [](double v) {
             const double e = exp(-fabs(v));
             const double rr = rcp(1.0 + e);
@@ -670,19 +693,15 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
           const bool badA = vA_all && pa.y > pa.N;
           const bool badB = PPL == 2 && vB_all && pb.y > pb.N;
           const bool bad = (__ballot(badA || badB) & slot_mask) != 0ull;
-          int idx = 0;
-          if (r == 0) idx = atomicAdd(ws + kWsReady, 1);
-          idx = __shfl(idx, leader);
-          double* e = ready + (int64_t)idx * kReadyStride;
-          const double v = r == 0 ? sig(u[0]) : (r == 1 ? sig(u[1]) : (r == 2 ? u[2] : exp(u[3]) + 2.0));
-          if (r < 4) __hip_atomic_store(e + r, bad ? NAN : v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (r == 4)
-            __hip_atomic_store(reinterpret_cast<uint64_t*>(e + 4), (uint64_t)taxon, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if (r == 5)
-            __hip_atomic_store(reinterpret_cast<uint64_t*>(e + 5), kReadyTag, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+          if (r == 0) {
+            const int idx = atomicAdd(ws + kWsReady, 1);
+            uint64_t* e = reinterpret_cast<uint64_t*>(ready + (int64_t)idx * kReadyStride);
+            ready_put(e + 0, bad ? NAN : sig(u[0]));
+            ready_put(e + 1, bad ? NAN : sig(u[1]));
+            ready_put(e + 2, bad ? NAN : u[2]);
+            ready_put(e + 3, bad ? NAN : exp(u[3]) + 2.0);
+            __hip_atomic_store(e + 4, ~(uint64_t)taxon, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
         }
         mode = kNextPair;
       } else if (mode == kPairFit) {
@@ -912,9 +931,11 @@ __global__ __launch_bounds__(kWave) void hpdi_prep_kernel(HpdiIO io, int64_t n_i
       // fit kernel (every entry written)
       const int64_t ei = item / io.per;
       const int i = (int)(item - ei * io.per);
-      const double* dg = io.ready + ei * kReadyStride;  // PMD-all: (q, A, c, phi, taxon, tag)
-      const double q = dg[0], A = dg[1], c = dg[2], phi = dg[3];
-      const int64_t t = (int64_t)__double_as_longlong(dg[4]);
+      // PMD-all: the complements of (q, A, c, phi, taxon) (ready_put)
+      const uint64_t* dg = reinterpret_cast<const uint64_t*>(io.ready + ei * kReadyStride);
+      const double q = __longlong_as_double(~dg[0]), A = __longlong_as_double(~dg[1]);
+      const double c = __longlong_as_double(~dg[2]), phi = __longlong_as_double(~dg[3]);
+      const int64_t t = (int64_t)~dg[4];
       oitem = t * io.per + i;
       N = (double)io.gN[t * kLD + i];
       if (N > 0.0 && !isnan(q)) {
@@ -993,26 +1014,41 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
 // per CU; the fit kernel's grid leaves them room), so the HPDI work fills the
 // fit kernel's idle issue slots and its tail; and one after fit_kernel on the
 // caller's stream, full occupancy, for what is left.
-// Waiting: a kEarly wave waits on entries only after it has seen fit_kernel's
-// started flag -- a started fit kernel completes whatever this kernel does,
-// and publishes all T entries -- and exits when the flag has not appeared
-// within ~50 us (its launch may have been queued behind this one: the two
-// streams can share a hardware queue); the late launch never waits.  Every
-// wave exits once the claim counter passes T * per.
+// Waiting (round 4: bounded, no wave waits indefinitely while holding a claim):
+// a kEarly wave waits on entries only after it has seen fit_kernel's started
+// flag, and exits when the flag has not appeared within ~50 us (its launch may
+// have been queued behind this one: the two streams can share a hardware
+// queue).  While it waits it holds claimed items; when a wave has made no
+// progress for `defer_ticks` (100 MHz ticks; MDFIT_STREAM_DEFER_US, default
+// 1 ms -- far beyond any wait of a co-resident run) or another
+// early wave has already deferred, it hands its pending items to the defer
+// list (reservation by CAS on kWsDefRes, one release add on kWsDefDone per
+// item written), claims no more, finishes its wide windows and exits -- so a
+// fit queue whose waves cannot get a slot (another kernel on the device, a
+// concurrent call) only delays the HPDI, it cannot hang the device.  The late
+// launch (after fit_kernel in stream order: every entry published) closes the
+// defer list (atomicOr of kDefClosed: a reservation after that fails, and the
+// early wave then keeps waiting -- fit_kernel is done, its entry is about to
+// be seen), waits until every reserved slot is written (its writer is
+// resident, one store away) and drains the deferred items after the main
+// claim counter.  The late launch never waits on the fit.
 #ifndef MDFIT_STREAM_WAVES_PER_CU
 #define MDFIT_STREAM_WAVES_PER_CU 4  // A/B at 10k and 125k taxa (tools/overlap_exp.py): 4 with the fit waves' base priority 1
 #endif
 template <bool kEarly>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPDI_WAVES_PER_EU))) void hpdi_stream_kernel(
     const uint32_t* __restrict__ gN, int64_t T, int per, double* __restrict__ out, float* __restrict__ pred,
-    int* __restrict__ ws, const double* __restrict__ ready) {
+    int* __restrict__ ws, const double* __restrict__ ready, int* __restrict__ defer, uint32_t defer_ticks) {
   const int lane = threadIdx.x;
+  uint64_t t_wait = 0;  // early: when the current run of trips without progress began (0: none)
   if (kEarly) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
     while (__hip_atomic_load(ws + kWsStarted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
       if (__builtin_amdgcn_s_memrealtime() - t0 > 5000u) return;  // 50 us: the fit kernel is not running
       __builtin_amdgcn_s_sleep(8);
     }
+    // another early wave has deferred already: nothing for this one to do
+    if (__hip_atomic_load(ws + kWsEarlyQuit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   }
   HpdiIO io{};
   io.out = out;
@@ -1026,17 +1062,49 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
   hpdi::Wide& W = sW[lane];
   int64_t item = 0, oitem = 0;  // the claimed item; its output index taxon * per + position
   bool busy = false, pending = false, drained = false;
+  // late launch: phase 0 claims from the main counter, phase 1 the deferred
+  // items (n_def of them, read once the list is closed); early: stop = this
+  // wave claims no more (it deferred, or saw another early wave defer),
+  // keep = the defer list is closed (keep waiting: every entry is published)
+  int phase = 0, n_def = -1;
+  bool stop = false, keep = false;
   while (true) {
-    const bool need = !busy && !pending && !drained;
+    const bool need = !busy && !pending && !drained && !stop;
     const unsigned long long m = __ballot(need);
     if (m != 0ull) {
       int base = 0;
-      if (lane == 0) base = atomicAdd(ws + kWsClaim, __popcll(m));
+      if (!kEarly && phase == 1) {
+        if (n_def < 0) {
+          // close the list; the count it held is final (reservations are CAS
+          // that fail once closed), then wait for its slots' writes.  A wave
+          // that finds it closed already reads the count with a plain load
+          // (one atomic per call, not per wave, on this line)
+          int r0 = 0;
+          if (lane == 0) {
+            r0 = __hip_atomic_load(ws + kWsDefRes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!(r0 & (int)kDefClosed)) r0 = atomicOr(ws + kWsDefRes, (int)kDefClosed);
+          }
+          n_def = __shfl(r0, 0) & ~(int)kDefClosed;
+          if (n_def > 0)
+            while (__hip_atomic_load(ws + kWsDefDone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < n_def)
+              __builtin_amdgcn_s_sleep(2);
+        }
+        if (lane == 0 && n_def > 0) base = atomicAdd(ws + kWsDefClaim, __popcll(m));
+      } else if (lane == 0) {
+        base = atomicAdd(ws + kWsClaim, __popcll(m));
+      }
       base = __shfl(base, 0);
       if (need) {
         const int64_t it = (int64_t)base + __popcll(m & ((1ull << lane) - 1ull));
-        if (it >= n_items) drained = true;
-        else {
+        if (!kEarly && phase == 1) {
+          if (n_def == 0 || it >= n_def) drained = true;
+          else {
+            item = __hip_atomic_load(defer + it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            pending = true;
+          }
+        } else if (it >= n_items) {
+          drained = true;
+        } else {
           item = it;
           pending = true;
         }
@@ -1046,15 +1114,28 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
     if (pending) {
       const int64_t ei = item / per;
       const double* e = ready + ei * kReadyStride;
-      const uint64_t tag = __hip_atomic_load(reinterpret_cast<const uint64_t*>(e + 5), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-      if (tag == kReadyTag) {
-        const double q = __hip_atomic_load(e + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const double A = __hip_atomic_load(e + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const double c = __hip_atomic_load(e + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const double phi = __hip_atomic_load(e + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int64_t taxon = (int64_t)__hip_atomic_load(reinterpret_cast<const uint64_t*>(e + 4), __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t* f = reinterpret_cast<const uint64_t*>(e);
+      // the taxon field first (written last), then the four values: taken when
+      // all five are non-zero (else the lane polls again next trip)
+#ifdef MDFIT_LOAD5
+      const uint64_t ftax = ready_get(f + 4);
+      const uint64_t fq = ready_get(f + 0), fA = ready_get(f + 1), fc = ready_get(f + 2), fphi = ready_get(f + 3);
+#else
+      const uint64_t ftax = ready_get(f + 4);
+      uint64_t fq = 0, fA = 0, fc = 0, fphi = 0;
+      if (ftax != 0) {
+        fq = ready_get(f + 0);
+        fA = ready_get(f + 1);
+        fc = ready_get(f + 2);
+        fphi = ready_get(f + 3);
+      }
+#endif
+      if (ftax != 0 && fq != 0 && fA != 0 && fc != 0 && fphi != 0) {
+        const double q = __longlong_as_double(~fq);
+        const double A = __longlong_as_double(~fA);
+        const double c = __longlong_as_double(~fc);
+        const double phi = __longlong_as_double(~fphi);
+        const int64_t taxon = (int64_t)~ftax;
         const int i = (int)(item - ei * per);
         // (never out of range: K0 zeroes the list and only this call's fit
         // kernel tags entries; a corrupt one is dropped and counted, not followed)
@@ -1077,7 +1158,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
         prog = true;
       }
     }
-    if (!__any(busy || pending || !drained)) break;
+    if (!kEarly && !__any(busy || pending || !drained)) {
+      if (phase == 1) break;
+      phase = 1;  // the main counter is drained: the deferred items
+      drained = false;
+      continue;
+    }
+    if (kEarly && !__any(busy || pending || (!drained && !stop))) break;
     if (busy) {
       prog = true;
       if (hpdi::wide_iter(W)) {
@@ -1087,7 +1174,51 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
         busy = false;
       }
     }
-    if (!__any(prog)) __builtin_amdgcn_s_sleep(8);  // every lane waits on an entry still being fitted
+    if (!__any(prog)) {  // every lane waits on an entry still being fitted
+#ifndef MDFIT_NO_DEFER
+      if (kEarly) {
+        // the clock is read only on trips without progress (it is a scalar
+        // memory round trip): t_wait = when this run of waiting began
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (t_wait == 0) t_wait = now;
+        // (the quit flag is read only by waves already waiting an eighth of
+        // the bound: a thousand waves polling one line slow every access to its
+        // L2 channel)
+        if (!keep && (now - t_wait > defer_ticks ||
+                      (now - t_wait > defer_ticks / 8 &&
+                       __hip_atomic_load(ws + kWsEarlyQuit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0))) {
+          const unsigned long long pm = __ballot(pending);
+          int base = -1;
+          if (lane == 0) {
+            int old = __hip_atomic_load(ws + kWsDefRes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while (!(old & (int)kDefClosed)) {
+              if (__hip_atomic_compare_exchange_strong(ws + kWsDefRes, &old, old + __popcll(pm), __ATOMIC_RELAXED,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                base = old;
+                break;
+              }
+            }
+          }
+          base = __shfl(base, 0);
+          if (base >= 0) {
+            if (pending) {
+              __hip_atomic_store(defer + base + __popcll(pm & ((1ull << lane) - 1ull)), (int)item, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_fetch_add(ws + kWsDefDone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+              pending = false;
+            }
+            if (lane == 0) __hip_atomic_store(ws + kWsEarlyQuit, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            stop = true;
+          } else {
+            keep = true;  // the late launch runs: fit_kernel is done, every entry is published
+          }
+        }
+      }
+#endif
+      __builtin_amdgcn_s_sleep(8);
+    } else {
+      t_wait = 0;
+    }
   }
 }
 
@@ -1246,6 +1377,11 @@ constexpr int kProfMax = 256;
 // beside the fit), the HPDI after the fit from 50-65k
 constexpr int64_t kPpl2MinTaxa = 13000;
 constexpr int64_t kStreamMaxTaxa = 60000;
+// the HPDI stream's defer list: one int32 per item an early wave hands back;
+// a wave defers at most once, at most its 64 lanes' items, so the early grid
+// is clamped to kDeferCap / 64 waves (2048: 8 per CU)
+constexpr int64_t kDeferCap = 131072;
+int64_t defer_cap(int64_t n_taxa) { return std::min<int64_t>(n_taxa * mdfit::kNPos, kDeferCap); }
 struct ProfState {
   bool on = false;
   bool fit_only = false;  // mdfit_profile_enable(2): only the events around fit_kernel
@@ -1418,8 +1554,10 @@ int64_t mdfit_workspace_bytes(int64_t n_taxa, const mdfit_opts* opts) {
   // the 256-byte header (counters, flags), then the ready list of
   // PMD-all modes (48 B per taxon); from kStreamMaxTaxa taxa (the HPDI after
   // the fit, K4a -> K4b) room for every position's wide-window record
+  // (+ the HPDI stream's defer list at the end)
   return 256 + n_taxa * mdfit::kReadyStride * (int64_t)sizeof(double) +
-         (n_taxa >= kStreamMaxTaxa ? n_taxa * mdfit::kNPos * (int64_t)sizeof(mdfit::hpdi::WideRec) : 0);
+         (n_taxa >= kStreamMaxTaxa ? n_taxa * mdfit::kNPos * (int64_t)sizeof(mdfit::hpdi::WideRec) : 0) +
+         defer_cap(n_taxa) * (int64_t)sizeof(int);
 }
 
 int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t n_taxa,
@@ -1476,11 +1614,17 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   if (const char* e = std::getenv("MDFIT_HPDI_STREAM")) stream = stream || std::atoi(e) != 0;
   const int early_per_cu =
       (fk != nullptr && stream) ? env_int("MDFIT_STREAM_WAVES_PER_CU", MDFIT_STREAM_WAVES_PER_CU) : 0;
+  // the defer list ends the workspace (mdfit_workspace_bytes); an early wave
+  // that waited defer_us without progress hands its items to the late launch
+  int* defer = reinterpret_cast<int*>(static_cast<char*>(workspace) + mdfit_workspace_bytes(n_taxa, &o) -
+                                      defer_cap(n_taxa) * (int64_t)sizeof(int));
+  const uint32_t defer_ticks = (uint32_t)std::max(0, env_int("MDFIT_STREAM_DEFER_US", 1000)) * 100u;
   ForkScope fork_hp(early_per_cu > 0 ? fk : nullptr, s, 0);
   if (early_per_cu > 0) {
-    const int64_t g = fit_grid(mdfit::hpdi_stream_kernel<true>, n_items, mdfit::kWave, early_per_cu);
+    const int64_t g = std::min<int64_t>(fit_grid(mdfit::hpdi_stream_kernel<true>, n_items, mdfit::kWave, early_per_cu),
+                                        kDeferCap / mdfit::kWave);
     hipLaunchKernelGGL(mdfit::hpdi_stream_kernel<true>, dim3((unsigned)g), dim3(mdfit::kWave), 0, fork_hp.side(), N,
-                       n_taxa, per, out, pred, ws, (const double*)ready);
+                       n_taxa, per, out, pred, ws, (const double*)ready, defer, defer_ticks);
     if (int rc = check_launch("hpdi_stream_kernel")) return rc;
   }
   prof_record(1, s);
@@ -1518,7 +1662,7 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
     const int64_t g = fit_grid(mdfit::hpdi_stream_kernel<false>, n_items, mdfit::kWave,
                                env_int("MDFIT_HPDI_WAVES_PER_CU", 0));
     hipLaunchKernelGGL(mdfit::hpdi_stream_kernel<false>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, N, n_taxa, per,
-                       out, pred, ws, (const double*)ready);
+                       out, pred, ws, (const double*)ready, defer, defer_ticks);
     if (int rc = check_launch("hpdi_stream_kernel")) return rc;
   } else {
     mdfit::HpdiIO io{};

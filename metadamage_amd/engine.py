@@ -209,8 +209,13 @@ def staging(capacity: int, device="cuda", opts: _lib.MdfitOpts | None = None, wi
         # x1.25 headroom from the first allocation on: the files of a run
         # differ in taxon count by a few %, and a regrow (pinned + device
         # buffers, ~0.15 s at 100k taxa) costs more than the spare memory
-        st = HostStaging(int(1.25 * max(int(capacity), st.capacity if st is not None else 0)), device=dev, opts=o,
-                         with_mm=with_mm)
+        cap = int(1.25 * max(int(capacity), st.capacity if st is not None else 0))
+        # (but not across the library's stream / after-the-fit HPDI switch: from
+        # 60k taxa the MAP workspace holds every position's wide-window record,
+        # ~4.8 KB per taxon that batches below 60k never touch)
+        if int(capacity) < _lib.STREAM_MAX_TAXA:
+            cap = min(cap, _lib.STREAM_MAX_TAXA - 1)
+        st = HostStaging(cap, device=dev, opts=o, with_mm=with_mm)
         _STAGING[key] = st
     return st
 

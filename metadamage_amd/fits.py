@@ -109,11 +109,12 @@ def pack_counts(df: pd.DataFrame, cfg) -> Packed:
     fwd, rev = cfg.substitution_bases_forward, cfg.substitution_bases_reverse
     tax = df["tax_id"]
     # taxon index in first-appearance order (pd.factorize) and each taxon's first row
-    if isinstance(tax.dtype, pd.CategoricalDtype) and len(tax.cat.categories) < 2**31:
+    codes = tax.cat.codes.to_numpy() if isinstance(tax.dtype, pd.CategoricalDtype) else None
+    if codes is not None and len(tax.cat.categories) < 2**31 and (codes.size == 0 or codes.min() >= 0):
         from . import ingest
 
-        t, first = ingest.first_index(tax.cat.codes.to_numpy(), len(tax.cat.categories))
-    else:
+        t, first = ingest.first_index(codes, len(tax.cat.categories))
+    else:  # (also a categorical holding a missing tax_id, code -1)
         t, _ = pd.factorize(tax.to_numpy())
         t = t.astype(np.int64)
         first = np.flatnonzero(np.r_[True, t[1:] > np.maximum.accumulate(t[:-1])]) if t.size else np.zeros(0, np.int64)

@@ -59,8 +59,8 @@ static long double hp_R(const hpd_t* P, double y) {
 /* ln p(x) - ln p(m) of the continuous extension (long double lgamma) */
 static double hp_g(const hpd_t* P, double x) {
   long double N = P->N, a = P->a, b = P->b, m = P->m, X = x;
-  long double r = (lgammal(X + a) - lgammal(m + a)) - (lgammal(X + 1.0L) - lgammal(m + 1.0L)) +
-                  (lgammal(N - X + b) - lgammal(N - m + b)) - (lgammal(N - X + 1.0L) - lgammal(N - m + 1.0L));
+  long double r = (o_lgammal(X + a) - o_lgammal(m + a)) - (o_lgammal(X + 1.0L) - o_lgammal(m + 1.0L)) +
+                  (o_lgammal(N - X + b) - o_lgammal(N - m + b)) - (o_lgammal(N - X + 1.0L) - o_lgammal(N - m + 1.0L));
   return (double)r;
 }
 

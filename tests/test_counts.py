@@ -60,6 +60,24 @@ def test_packing_matches_group_to_numpyro_data(name, ref_meta, ref_golden):
     assert (p.mm == mm).all()
 
 
+def test_packing_categorical_with_a_missing_tax_id(ref_meta):
+    """A categorical tax_id column holding a missing value (code -1) packs like
+    the same column as plain values (the pd.factorize path), not through the
+    first-appearance index of non-negative codes."""
+    name = list(CASES)[0]
+    cfg = cfg_for(ref_meta["cases"][name], GOLDEN / CASES[name])
+    df = pd.read_parquet(GOLDEN / f"counts_{name}.parquet")
+    df["tax_id"] = df["tax_id"].astype(str).astype(object)
+    df.loc[df.index[-30:], "tax_id"] = np.nan  # the last taxon's rows
+    plain = fits.pack_counts(df, cfg)
+    cat = df.copy()
+    cat["tax_id"] = cat["tax_id"].astype("category")
+    assert cat["tax_id"].cat.codes.min() == -1
+    p = fits.pack_counts(cat, cfg)
+    assert p.n_taxa == plain.n_taxa
+    assert (p.y == plain.y).all() and (p.N == plain.N).all()
+
+
 def test_top_max_fits_matches_reference(ref_meta):
     for name in CASES:
         df = pd.read_parquet(GOLDEN / f"counts_{name}.parquet")

@@ -70,7 +70,7 @@ def test_c3_nuts_100k(engine, oracle_lib):
     res = engine.fit_batch_device(ty, tN, tm, opts)
     torch.cuda.synchronize()
     out, st = res.out.cpu().numpy(), res.status.cpu().numpy()
-    assert (st == 0).mean() > 0.999
+    assert (st == 0).all(), np.flatnonzero(st != 0)[:10]  # every taxon OK (as in every box run so far)
     assert np.isfinite(out[st == 0][:, [0, 1, 4, 5, 6, 15, 18, 21]]).all()
     sub = 30_000 + np.arange(64)  # a contiguous subsample (one oracle call, index_base keyed)
     smp = engine.samples_view(res, T, opts)[torch.as_tensor(sub, device=res.out.device)].cpu().numpy()

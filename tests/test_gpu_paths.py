@@ -10,7 +10,9 @@ call bit for bit:
     serialised by a mutex);
   * the call captured into a HIP graph and replayed;
   * garbage-filled workspace and outputs (MAP in both layouts, NUTS): every
-    record column equal to a call on zeroed buffers.
+    record column equal to a call on zeroed buffers;
+  * the HPDI stream beside the fit, its defer path forced, and two calls on two
+    streams at once beside unrelated kernels.
 """
 
 from __future__ import annotations
@@ -189,13 +191,24 @@ def test_hpdi_stream_beside_the_fit_same_record(torch_dev, monkeypatch, ppl):
     ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm)
     opts = _lib.default_opts()
     recs = []
-    for early in ("0", "2", "4"):
-        monkeypatch.setenv("MDFIT_STREAM_WAVES_PER_CU", early)
+    # "4d": the early waves defer every item they would wait on (MDFIT_STREAM_DEFER_US=0):
+    # the late launch drains them from the defer list
+    for early in ("0", "2", "4", "4d"):
+        monkeypatch.setenv("MDFIT_STREAM_WAVES_PER_CU", early[0])
+        monkeypatch.setenv("MDFIT_STREAM_DEFER_US", "0" if early == "4d" else "1000")
         for with_pred in (True, False):
             r = engine.fit_batch_device(ty, tN, tm, opts, engine.alloc_outputs(4_000, with_pred=with_pred, opts=opts))
             torch.cuda.synchronize()
             hdr = r.workspace[:256].view(torch.int32).cpu().numpy()
             assert hdr[8] == 4_000 and hdr[11] == 0  # one ready entry per taxon, no corrupt entry met
+            n_def = hdr[32] & ~0x40000000
+            if early != "0":
+                assert hdr[32] & 0x40000000  # the late launch closed the defer list
+                assert hdr[33] == n_def and hdr[34] >= n_def  # every reserved slot written, and drained
+            if early == "4d":
+                assert n_def > 0 and hdr[35] == 1
+            else:
+                assert n_def == 0  # an undisturbed call never waits 1 ms
             recs.append((early, with_pred, r.out.cpu().numpy()[:, :32], None if r.pred is None else r.pred.cpu().numpy(),
                          r.status.cpu().numpy()))
     base = {wp: rec for e, wp, *rec in recs if e == "0"}
@@ -206,3 +219,42 @@ def test_hpdi_stream_beside_the_fit_same_record(torch_dev, monkeypatch, ppl):
         if wp:
             assert np.array_equal(pred, p0, equal_nan=True), (e, wp)
     assert np.isfinite(base[True][0][:, 2:4]).mean() > 0.99
+
+
+def test_two_calls_on_two_streams_at_once(torch_dev):
+    """Two MAP calls enqueued on two streams back to back, beside a third stream
+    busy with unrelated kernels: the HPDI stream's early waves may then find
+    their fit kernel short of slots, and must not wait on it indefinitely
+    (bounded waits, the defer list).  Each call gives the record of
+    the same call run alone, bit for bit."""
+    torch = torch_dev
+    from metadamage_amd import _lib, engine
+    from metadamage_amd.synthetic import generate
+
+    opts = _lib.default_opts()
+    lib = _lib.load()
+    cases = []
+    for T, seed in ((6_000, 31), (20_000, 32)):  # both lane layouts
+        b = generate(T, seed=seed)
+        ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm)
+        ref = engine.fit_batch_device(ty, tN, tm, opts)
+        torch.cuda.synchronize()
+        cases.append((T, ty, tN, tm, ref))
+    a = torch.randn(4096, 4096, device="cuda")
+    busy = torch.cuda.Stream()
+    streams = [torch.cuda.Stream() for _ in cases]
+    for rep in range(3):
+        res = [engine.alloc_outputs(T, opts=opts) for T, *_ in cases]
+        torch.cuda.synchronize()
+        with torch.cuda.stream(busy):
+            for _ in range(8):
+                a = torch.tanh(a @ a * 1e-3)
+        for (T, ty, tN, tm, _), r, s in zip(cases, res, streams):
+            _call(lib, ty, tN, tm, T, opts, r, ctypes.c_void_p(s.cuda_stream))
+        torch.cuda.synchronize()
+        for (T, ty, tN, tm, ref), r in zip(cases, res):
+            assert np.array_equal(r.out.cpu().numpy()[:, :32], ref.out.cpu().numpy()[:, :32], equal_nan=True), (rep, T)
+            assert np.array_equal(r.pred.cpu().numpy(), ref.pred.cpu().numpy(), equal_nan=True), (rep, T)
+            assert np.array_equal(r.status.cpu().numpy(), ref.status.cpu().numpy()), (rep, T)
+            hdr = r.workspace[:256].view(torch.int32).cpu().numpy()
+            assert hdr[8] == T and hdr[11] == 0

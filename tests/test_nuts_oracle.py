@@ -12,6 +12,8 @@ numpyro / jax cannot run here, so the sampler is pinned by:
 
 from __future__ import annotations
 
+from pathlib import Path
+
 import numpy as np
 import pytest
 from scipy.special import gammaln
@@ -234,3 +236,13 @@ def test_adaptation_windows(nw, expect):
         return out
 
     assert schedule(nw) == expect
+
+
+def test_nuts_columns_fixture_reproduces(oracle_lib):
+    """tests/golden/nuts_columns_oracle.npz (the GPU test's reference) is the
+    committed oracle's output: two of its taxa re-run under one of its seeds."""
+    g = np.load(Path(__file__).resolve().parent / "golden" / "nuts_columns_oracle.npz")
+    si = 3
+    out, _, st = oracle_lib.nuts_batch(g["y"][:2], g["N"][:2], g["mm"][:2], seed=int(g["seeds"][si]), threads=2)
+    assert (st == g["status"][si][:2]).all()
+    assert np.array_equal(out[:, :25], g["out"][si][:2], equal_nan=True)
