@@ -283,8 +283,21 @@ def main():
 
     if rank == 0 and nuts:
         smp = engine.samples_view(fb, T, opts)[:64].cpu().numpy()
-        print(json.dumps(nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, b, smp)),
-              flush=True)
+        # the chain kernel's counters of the last call (workspace header, uint64
+        # at byte 128 / 136): wave-trips with a running slot, running slot-trips
+        util = fb.workspace[128:144].view(torch.int64).cpu().numpy()
+        # compute roofline: register-only probe of the same potential evaluation
+        n_waves, iters = 256 * 20, 32
+        engine.peak_probe(n_waves, iters, stream=stream, nuts=True)  # warm
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(3):
+            engine.peak_probe(n_waves, iters, stream=stream, nuts=True)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        probe_rate = 3 * n_waves * 60 * iters / (e0.elapsed_time(e1) / 1e3)  # 60 points per wave-iteration
+        print(json.dumps(nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, b, smp,
+                                   util, probe_rate)), flush=True)
     elif rank == 0:
         value = total_per_step * args.steps / elapsed
         k_avg_s = fit_ms_sum / n_calls / 1e3
@@ -425,7 +438,7 @@ def host_to_host(engine, b, opts, dev, steps: int) -> dict:
     return out
 
 
-def nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, b, smp):
+def nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, b, smp, util, probe_rate):
     """The JSON line of config C3 (the reference's NUTS, 500 warmup + 1000 draws
     per sub-fit, 6 sub-fits per taxon)."""
     from metadamage_amd import _lib
@@ -483,6 +496,18 @@ def nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, 
                 "diagnostics out -- the hand-off to nuts_post_kernel",
             },
             "call_ms_avg": round(call_ms_sum / n_calls, 3),
+        },
+        "compute_roofline": {
+            "bound": "fp64-valu",
+            "achieved": round(15.0 * float(util[1]) / k_avg_s, 1),
+            "peak": round(probe_rate, 1),
+            "unit": "point-evals/s",
+            "frac": 15.0 * float(util[1]) / k_avg_s / probe_rate,
+            "slot_util": float(util[1]) / max(1.0, 4.0 * float(util[0])),
+            "point_evals_per_taxon": 15.0 * float(util[1]) / T,
+            "note": "the chain kernel's potential evaluations (15 points per running chain slot per trip: "
+            "leapfrogs, initial points, step-size probes; counted by the kernel) / its time, against "
+            "nuts_probe_kernel, a register-only loop over the same potential_cd at the chain kernel's occupancy",
         },
         "leapfrog_point_evals_per_s": round(point_evals / k_avg_s, 1),
         "mean_leapfrogs_per_iteration": round(float(leap.mean()), 3),

@@ -217,6 +217,14 @@ int mdfit_objective(const int32_t* model, const int32_t* subset, const uint32_t*
 int mdfit_peak_probe(int64_t n_waves, int32_t iters, double* sink, void* hip_stream);
 
 /*
+ * The same for the sampling mode: the chain kernel's potential evaluation
+ * (value + gradient of 15 beta-binomial points per 16-lane chain slot, the
+ * unconstrained transform, the row sums) at the chain kernel's occupancy;
+ * 60 point-evaluations per wave-iteration.  bench.py's NUTS compute roofline.
+ */
+int mdfit_nuts_peak_probe(int64_t n_waves, int32_t iters, double* sink, void* hip_stream);
+
+/*
  * Sampling-mode potential -(log density + log|J|) and its gradient in the
  * unconstrained v = (logit q, logit A, logit c, log delta) (numpyro's
  * potential of model_PMD / model_null, fits.py:43-67), evaluated by the chain

@@ -69,6 +69,7 @@ EXPORTED_SYMBOLS = [
     "mdfit_special",
     "mdfit_hpdi68",
     "mdfit_peak_probe",
+    "mdfit_nuts_peak_probe",
     "mdfit_objective",
     "mdfit_nuts_potential",
     "mdfit_profile_enable",
@@ -140,6 +141,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.mdfit_hpdi68.restype = ctypes.c_int
     lib.mdfit_peak_probe.argtypes = [i64, i32, vp, vp]
     lib.mdfit_peak_probe.restype = ctypes.c_int
+    lib.mdfit_nuts_peak_probe.argtypes = [i64, i32, vp, vp]
+    lib.mdfit_nuts_peak_probe.restype = ctypes.c_int
     lib.mdfit_objective.argtypes = [vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp]
     lib.mdfit_objective.restype = ctypes.c_int
     lib.mdfit_last_error.argtypes = []

@@ -1763,6 +1763,11 @@ int mdfit_nuts_potential(const int32_t* model, const int32_t* subset, const uint
   return mdfit::nuts::potential(model, subset, y, N, v, n, U, g, (hipStream_t)hip_stream);
 }
 
+int mdfit_nuts_peak_probe(int64_t n_waves, int32_t iters, double* sink, void* hip_stream) {
+  if (n_waves <= 0 || iters <= 0 || !sink) return set_err(MDFIT_E_ARG, "bad arguments");
+  return mdfit::nuts::peak_probe(n_waves, iters, sink, (hipStream_t)hip_stream);
+}
+
 const char* mdfit_last_error(void) { return g_err; }
 
 int mdfit_abi_version(void) { return MDFIT_ABI_VERSION; }

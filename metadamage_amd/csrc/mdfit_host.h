@@ -63,6 +63,8 @@ namespace mdfit::nuts {
 // the chains' samples double[T][6][num_samples][4] = (q, A, c, phi)
 constexpr int64_t kSamplesOffset = 256;
 int64_t workspace_bytes(int64_t n_taxa, int num_samples);
+// register-only throughput probe of the chain kernel's potential evaluation
+int peak_probe(int64_t n_waves, int iters, double* sink, hipStream_t s);
 int potential(const int32_t* model, const int32_t* subset, const uint32_t* y, const uint32_t* N, const double* v,
               int64_t n, double* U, double* g, hipStream_t s);
 // launches the chain and post-processing kernels (workspace already zeroed)

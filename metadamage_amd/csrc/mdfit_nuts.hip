@@ -1358,7 +1358,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   double s_w = 0.0, s_acc = 0.0;
   int leaf_ctr = 0, nleap = 0, s_n = 0, n_leaf = 0, nmax = 1, ul_chunk = -1;
   int right = 1, t_turn = 0, t_div = 0, s_div = 0;
-#ifdef MDFIT_DEV_UTIL
+// slot utilisation and the point-evaluation count (bench.py's compute
+// roofline): wave-trips with a running slot, and running slot-trips (each one
+// potential evaluation of 15 points), added into the workspace header
+// (uint64 at byte 128 / 136; zeroed per call) when the wave exits
+#ifndef MDFIT_NO_UTIL
   unsigned long long util_trips = 0, util_busy = 0;
 #endif
 
@@ -1438,7 +1442,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
     if (!__any(mode != 0 || !drained)) break;
     const bool running = mode == kInit || mode == kFind || mode == kIter;
     if (!__any(running)) continue;
-#ifdef MDFIT_DEV_UTIL  // development: slot utilisation (trips with a running slot / all slot-trips)
+#ifndef MDFIT_NO_UTIL
     {
       const unsigned long long rb = __ballot(running && i == 0);
       util_trips += 1;
@@ -1790,7 +1794,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       step = right ? C.eps : -C.eps;
     }
   }
-#ifdef MDFIT_DEV_UTIL
+#ifndef MDFIT_NO_UTIL
   if (threadIdx.x == 0) {
     atomicAdd(reinterpret_cast<unsigned long long*>(ws + 32), util_trips);
     atomicAdd(reinterpret_cast<unsigned long long*>(ws + 34), util_busy);
@@ -2207,6 +2211,40 @@ __global__ __launch_bounds__(kWave) void nuts_potential_kernel(const int32_t* __
 // ---------------------------------------------------------------------------
 // host
 // ---------------------------------------------------------------------------
+// Register-only throughput probe of the sampler's point evaluation: the chain
+// kernel's potential_cd (value + gradient of 15 points per 16-lane slot, the
+// transform of the position, the five row sums) in the chain kernel's lane
+// layout and at its occupancy (MDFIT_NUTS_CD_WAVES waves per SIMD), on a
+// representative argument mix (a = D phi below 10: the shifted lnGamma, the
+// others not -- as in typical chains).  Useful work: 60 point-evaluations per
+// wave-iteration (4 slots x 15 points), the unit of bench.py's NUTS
+// compute_roofline.
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUTS_CD_WAVES))) void nuts_probe_kernel(
+    int iters, double* __restrict__ sink) {
+  const int lane = threadIdx.x;
+  const int i = lane & 15;
+  PointData pd[1];
+  pd[0].valid = i < kNHalf;
+  pd[0].pmd = true;
+  pd[0].k = pd[0].valid ? i : 0;
+  pd[0].N = pd[0].valid ? 1.0e5 + 1000.0 * lane : 0.0;
+  pd[0].y = 0.01 * pd[0].N;
+  const int c = lane & 3;
+  double x = c == 0 ? -0.5 : (c == 1 ? -3.0 : (c == 2 ? -4.0 : 6.0));
+  double acc = 0.0;
+  for (int it = 0; it < iters; ++it) {
+    const PotC P = potential_cd<1>(pd, x, false);
+    acc += P.U;
+    x += 1e-12 * P.g;  // loop-carried: no hoisting
+  }
+  sink[(int64_t)blockIdx.x * kWave + lane] = acc + x;
+}
+
+int peak_probe(int64_t n_waves, int iters, double* sink, hipStream_t s) {
+  hipLaunchKernelGGL(nuts_probe_kernel, dim3((unsigned)n_waves), dim3(kWave), 0, s, iters, sink);
+  return host::check_launch("nuts_probe_kernel");
+}
+
 int potential(const int32_t* model, const int32_t* subset, const uint32_t* y, const uint32_t* N, const double* v,
               int64_t n, double* U, double* g, hipStream_t s) {
   if (n == 0) return 0;

@@ -155,24 +155,30 @@ class HostStaging:
         self.d_mm = torch.empty((T, _lib.NPOS, _lib.NMM), dtype=torch.int32, device=self.device) if with_mm else None
         self.res = alloc_outputs(T, device=self.device, with_pred=with_pred, opts=opts)
 
-    def run(self, y, N, mm=None, opts: _lib.MdfitOpts | None = None, stream=None, sync: bool = True):
+    def run(self, y, N, mm=None, opts: _lib.MdfitOpts | None = None, stream=None, sync: bool = True,
+            pinned: PinnedPack | None = None):
         """Fit the first len(y) taxa; returns numpy views (out[:, :32], pred,
-        status) of the pinned buffers (valid until the next run)."""
+        status) of the pinned buffers (valid until the next run).  pinned: y,
+        N, mm are that PinnedPack's views, copied to the device from there."""
         torch = _torch()
         T = int(y.shape[0])
         if T > self.capacity:
             raise ValueError(f"{T} taxa > staging capacity {self.capacity}")
-        self.h_y[:T].numpy()[:] = np.asarray(y, dtype=np.uint32).view(np.int32)
-        self.h_N[:T].numpy()[:] = np.asarray(N, dtype=np.uint32).view(np.int32)
         use_mm = mm is not None and self.h_mm is not None
-        if use_mm:
-            self.h_mm[:T].numpy()[:] = np.asarray(mm, dtype=np.uint32).view(np.int32)
+        if pinned is not None:
+            src_y, src_N, src_mm = pinned.h_y[:T], pinned.h_N[:T], pinned.h_mm[:T]
+        else:
+            self.h_y[:T].numpy()[:] = np.asarray(y, dtype=np.uint32).view(np.int32)
+            self.h_N[:T].numpy()[:] = np.asarray(N, dtype=np.uint32).view(np.int32)
+            if use_mm:
+                self.h_mm[:T].numpy()[:] = np.asarray(mm, dtype=np.uint32).view(np.int32)
+            src_y, src_N, src_mm = self.h_y[:T], self.h_N[:T], self.h_mm[:T] if use_mm else None
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         with torch.cuda.stream(s):
-            self.d_y[:T].copy_(self.h_y[:T], non_blocking=True)
-            self.d_N[:T].copy_(self.h_N[:T], non_blocking=True)
+            self.d_y[:T].copy_(src_y, non_blocking=True)
+            self.d_N[:T].copy_(src_N, non_blocking=True)
             if use_mm:
-                self.d_mm[:T].copy_(self.h_mm[:T], non_blocking=True)
+                self.d_mm[:T].copy_(src_mm, non_blocking=True)
             res = FitBatch(self.res.out[:T], self.res.pred[:T] if self.res.pred is not None else None,
                            self.res.status[:T], self.res.workspace)
             fit_batch_device(self.d_y[:T], self.d_N[:T], self.d_mm[:T] if use_mm else None, opts, res, stream=s)
@@ -184,6 +190,59 @@ class HostStaging:
             s.synchronize()
         pred = self.h_pred[:T].numpy() if self.h_pred is not None else None
         return self.h_out[:T].numpy(), pred, self.h_status[:T].numpy()
+
+
+class PinnedPack:
+    """A pinned host buffer set for one file's packed counts (y, N: uint32
+    [cap][32], mm: uint32[cap][30][12]): fits.pack_counts writes into it on a
+    reader thread and HostStaging.run copies it to the device directly (no
+    host copy into the staging buffers: ~170 MB per 100k-taxon file)."""
+
+    def __init__(self, capacity: int):
+        torch = _torch()
+        self.capacity = int(capacity)
+        T = self.capacity
+        self.h_y = torch.empty((T, _lib.LD), dtype=torch.int32).pin_memory()
+        self.h_N = torch.empty((T, _lib.LD), dtype=torch.int32).pin_memory()
+        self.h_mm = torch.empty((T, _lib.NPOS, _lib.NMM), dtype=torch.int32).pin_memory()
+
+    def views(self, T: int):
+        """numpy uint32 views (y, N, mm) of the first T taxa."""
+        return (self.h_y[:T].numpy().view(np.uint32), self.h_N[:T].numpy().view(np.uint32),
+                self.h_mm[:T].numpy().view(np.uint32))
+
+
+_PINNED_FREE: list = []
+_PINNED_N = 0
+_PINNED_MAX = 3  # files in flight in main.main: N_READERS ahead + the one being fitted
+_PINNED_LOCK = __import__("threading").Lock()
+
+
+def acquire_pinned_pack(T: int) -> PinnedPack | None:
+    """A free PinnedPack of at least T taxa (x1.25 headroom when one is made),
+    or None when every set is in use (the caller then packs into pageable
+    memory) or no HIP device is visible."""
+    import torch
+
+    if not torch.cuda.is_available():
+        return None
+    global _PINNED_N
+    with _PINNED_LOCK:
+        for i, pp in enumerate(_PINNED_FREE):
+            if pp.capacity >= T:
+                return _PINNED_FREE.pop(i)
+        if _PINNED_FREE:  # too small: replaced by a larger one
+            _PINNED_FREE.pop(0)
+            _PINNED_N -= 1
+        if _PINNED_N >= _PINNED_MAX:
+            return None
+        _PINNED_N += 1
+    return PinnedPack(int(1.25 * T) + 1)
+
+
+def release_pinned_pack(pp: PinnedPack) -> None:
+    with _PINNED_LOCK:
+        _PINNED_FREE.append(pp)
 
 
 _STAGING: dict = {}
@@ -220,13 +279,15 @@ def staging(capacity: int, device="cuda", opts: _lib.MdfitOpts | None = None, wi
     return st
 
 
-def fit_batch_host(y, N, mm=None, opts: _lib.MdfitOpts | None = None, noise=None, device="cuda"):
+def fit_batch_host(y, N, mm=None, opts: _lib.MdfitOpts | None = None, noise=None, device="cuda",
+                   pinned: PinnedPack | None = None):
     """The product's host-to-host fit: (out[T, 32], pred, status).  mm goes
     to the device (the assembly computes the noise columns); without it,
-    `noise` (float64[T][3], ingest.noise) fills them when given."""
+    `noise` (float64[T][3], ingest.noise) fills them when given.  pinned: y,
+    N, mm are views of that PinnedPack (copied to the device from there)."""
     with _STAGING_LOCK:
         st = staging(int(np.asarray(y).shape[0]), device=device, opts=opts, with_mm=mm is not None)
-        out, pred, status = st.run(y, N, mm, opts)
+        out, pred, status = st.run(y, N, mm, opts, pinned=pinned if mm is not None else None)
         out, pred, status = out.copy(), pred.copy(), status.copy()
     if mm is None and noise is not None:
         ok = status != _lib.INVALID
@@ -279,12 +340,15 @@ def hpdi68(N, a, b, device="cuda"):
     return lo.cpu().numpy(), hi.cpu().numpy()
 
 
-def peak_probe(n_waves: int, iters: int, stream=None):
-    """Launch the register-only point-evaluation probe; returns the sink tensor."""
+def peak_probe(n_waves: int, iters: int, stream=None, nuts: bool = False):
+    """Launch the register-only point-evaluation probe (MAP: value + gradient +
+    Hessian; nuts: the sampler's potential, value + gradient); returns the sink
+    tensor."""
     torch = _torch()
     lib = _lib.load()
     sink = torch.empty(n_waves * 64, dtype=torch.float64, device="cuda")
-    _lib.check(lib.mdfit_peak_probe(n_waves, iters, ctypes.c_void_p(sink.data_ptr()), _stream_handle(torch, stream)))
+    fn = lib.mdfit_nuts_peak_probe if nuts else lib.mdfit_peak_probe
+    _lib.check(fn(n_waves, iters, ctypes.c_void_p(sink.data_ptr()), _stream_handle(torch, stream)))
     return sink
 
 

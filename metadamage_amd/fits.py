@@ -46,7 +46,7 @@ INT_RESULT_FIELDS = {"N_alignments", "N_z1_forward", "N_z1_reverse", "N_sum_forw
 # packing: df_counts -> dense [T][32] tensors (batched group_to_numpyro_data)
 # --------------------------------------------------------------------------
 class Packed:
-    def __init__(self, tax_id, tax_name, tax_rank, N_alignments, y, N, mm, cats=None):
+    def __init__(self, tax_id, tax_name, tax_rank, N_alignments, y, N, mm, cats=None, pinned=None):
         self.tax_id = tax_id
         self.tax_name = tax_name
         self.tax_rank = tax_rank
@@ -58,6 +58,18 @@ class Packed:
         # had them (sorted categories): the frames reuse their order instead of
         # re-sorting a million names
         self.cats = cats or {}
+        # the engine.PinnedPack y / N / mm live in (main.main's pipeline), handed
+        # back to its pool once the device has them (release_pinned)
+        self.pinned = pinned
+
+    def release_pinned(self):
+        """Return the pinned buffer set; y / N / mm are gone afterwards."""
+        if self.pinned is not None:
+            from . import engine
+
+            engine.release_pinned_pack(self.pinned)
+            self.pinned = None
+            self.y = self.N = self.mm = None
 
     @property
     def n_taxa(self):
@@ -96,7 +108,7 @@ def _first_categoricals(df: pd.DataFrame, first: np.ndarray) -> dict:
     return out
 
 
-def pack_counts(df: pd.DataFrame, cfg) -> Packed:
+def pack_counts(df: pd.DataFrame, cfg, pinned: bool = False) -> Packed:
     """Dense y/N (uint32[T][32]) and mismatch counts (uint32[T][30][12]) in
     df order (first appearance of each tax_id, i.e. the N_alignments-desc
     order of sort_by_alignments).  Column i < 15 holds z = i+1 (y = the
@@ -128,9 +140,19 @@ def pack_counts(df: pd.DataFrame, cfg) -> Packed:
     dense = n == T * _lib.NPOS and np.array_equal(
         pos.reshape(T, _lib.NPOS), np.broadcast_to(POSITIONS.astype(pos.dtype), (T, _lib.NPOS))) and np.array_equal(
         t.reshape(T, _lib.NPOS), np.broadcast_to(np.arange(T)[:, None], (T, _lib.NPOS)))
-    y = np.zeros((T, _lib.LD), np.uint32)
-    N = np.zeros((T, _lib.LD), np.uint32)
-    mm = np.empty((T, _lib.NPOS, _lib.NMM), np.uint32)
+    pp = None
+    if pinned and T > 0:  # straight into a pinned buffer set (pinned=True: main.main's reader threads)
+        from . import engine
+
+        pp = engine.acquire_pinned_pack(T)
+    if pp is not None:
+        y, N, mm = pp.views(T)
+        y.fill(0)
+        N.fill(0)
+    else:
+        y = np.zeros((T, _lib.LD), np.uint32)
+        N = np.zeros((T, _lib.LD), np.uint32)
+        mm = np.empty((T, _lib.NPOS, _lib.NMM), np.uint32)
     if dense:
         y[:, :_lib.NPOS] = yv.reshape(T, _lib.NPOS)
         N[:, :_lib.NPOS] = Nv.reshape(T, _lib.NPOS)
@@ -156,6 +178,7 @@ def pack_counts(df: pd.DataFrame, cfg) -> Packed:
         N=N,
         mm=mm,
         cats=_first_categoricals(df, first),
+        pinned=pp,
     )
 
 
@@ -188,7 +211,9 @@ def fit_packed(p: Packed, opts=None, shard: bool = True):
     # statistics (ingest.noise) take ~1.5 ms of CPU per 10k taxa on the 16-thread
     # share of a multi-file pipeline that is host-bound
     if not grouped:
-        return engine.fit_batch_host(p.y, p.N, p.mm, opts)
+        res = engine.fit_batch_host(p.y, p.N, p.mm, opts, pinned=p.pinned)
+        p.release_pinned()  # (the call synchronised: the device has the counts)
+        return res
     lo, hi = shard_range(p.n_taxa, rank, world)
     if opts is not None:  # the sampler's streams are keyed by the global taxon index
         opts = _lib.MdfitOpts.from_buffer_copy(opts)
@@ -198,6 +223,8 @@ def fit_packed(p: Packed, opts=None, shard: bool = True):
     if hi > lo:
         ty, tN, tm = engine.to_device_counts(p.y[lo:hi], p.N[lo:hi], p.mm[lo:hi] if p.mm is not None else None,
                                              device=dev)
+    p.release_pinned()  # (to_device_counts copied synchronously)
+    if hi > lo:
         engine.fit_batch_device(ty, tN, tm, opts, engine.FitBatch(rec.out[: hi - lo], rec.pred[: hi - lo],
                                                                    rec.status[: hi - lo]))
     buf = rec.stage()
@@ -212,13 +239,28 @@ def fit_packed(p: Packed, opts=None, shard: bool = True):
 # frames (fits.py:632-680)
 # --------------------------------------------------------------------------
 def _category(p: Packed, name: str, keep, repeat: int = 1) -> pd.Categorical:
-    """astype("category") of np.repeat(getattr(p, name)[keep], repeat):
+    """astype("category") of np.repeat(getattr(p, name)[keep], repeat) (keep
+    None: every taxon):
     categories = the sorted distinct values.  From the packed categorical when
     there is one (its categories are sorted already), else by factorising the
     per-taxon values once (the predictions repeat each taxon 30 times)."""
     cat = p.cats.get(name)
-    c = cat[keep].remove_unused_categories() if cat is not None else pd.Categorical(getattr(p, name)[keep])
-    return pd.Categorical.from_codes(np.repeat(c.codes, repeat), c.categories) if repeat != 1 else c
+    if cat is None:
+        v = getattr(p, name)
+        c = pd.Categorical(v if keep is None else v[keep])
+    else:
+        # remove_unused_categories by a presence table instead of np.unique's
+        # sort (the categories stay in their sorted order)
+        codes = cat.codes if keep is None else cat.codes[keep]
+        used = np.zeros(len(cat.categories), bool)
+        used[codes[codes >= 0]] = True
+        if used.all():
+            c = pd.Categorical.from_codes(codes, dtype=cat.dtype)
+        else:
+            remap = (np.cumsum(used) - 1).astype(codes.dtype)
+            c = pd.Categorical.from_codes(np.where(codes >= 0, remap[np.maximum(codes, 0)], -1).astype(codes.dtype),
+                                          cat.categories[used])
+    return pd.Categorical.from_codes(np.repeat(c.codes, repeat), dtype=c.dtype) if repeat != 1 else c
 
 
 def _const_category(value, n: int) -> pd.Categorical:
@@ -232,33 +274,51 @@ def _uint32(v: np.ndarray) -> np.ndarray:
     return v.astype(np.uint32)
 
 
+def _record_columns(out, keep, ncol: int, block: int = 2048) -> np.ndarray:
+    """The first ncol columns of the kept rows of the row-major record as a
+    column-major float64[ncol][n], transposed block by block (a column gathered
+    from the 640-B record rows touches one cache line per taxon; a whole-array
+    transposed copy ~4x slower than these cache-sized blocks)."""
+    idx = None if keep is None else np.flatnonzero(keep)
+    n = out.shape[0] if idx is None else idx.size
+    cols = np.empty((ncol, n), np.float64)
+    for i in range(0, n, block):
+        rows = out[i:i + block, :ncol] if idx is None else out[idx[i:i + block], :ncol]
+        cols[:, i:i + block] = rows.T
+    return cols
+
+
 def make_df_fit_results(p: Packed, out, keep, cfg) -> pd.DataFrame:
     """One row per fitted taxon in FIT_RESULT_COLUMNS order with the dtypes of
     downcast_dataframe (fits.py:668-680 + utils.py:329-356): names
     categorical, integer fields uint32, the rest float32."""
+    n = int(keep.sum())
+    keep = None if n == len(keep) else keep  # (every taxon kept: no row selection)
     data = {
         "tax_id": _category(p, "tax_id", keep),
         "tax_name": _category(p, "tax_name", keep),
         "tax_rank": _category(p, "tax_rank", keep),
     }
+    cols = _record_columns(out, keep, _lib.NRESULT)
     for j, name in enumerate(_lib.RESULT_FIELDS):
-        v = out[keep, j]
+        v = cols[j]
         data[name] = _uint32(np.rint(v).astype(np.int64)) if name in INT_RESULT_FIELDS else v.astype(np.float32)
-    data["N_alignments"] = _uint32(p.N_alignments[keep])
-    data["shortname"] = _const_category(cfg.shortname, int(keep.sum()))
+    data["N_alignments"] = _uint32(p.N_alignments if keep is None else p.N_alignments[keep])
+    data["shortname"] = _const_category(cfg.shortname, n)
     return pd.DataFrame({c: data[c] for c in FIT_RESULT_COLUMNS}, copy=False)
 
 
 def make_df_fit_predictions(p: Packed, pred, keep, cfg) -> pd.DataFrame:
     """fits.py:632-665: 30 rows per fitted taxon (z = 1..15, -1..-15)."""
     n = int(keep.sum())
+    kp = pred if n == len(keep) else pred[keep]
     return pd.DataFrame(
         {
-            "tax_id": _category(p, "tax_id", keep, _lib.NPOS),
+            "tax_id": _category(p, "tax_id", None if n == len(keep) else keep, _lib.NPOS),
             "position": np.tile(POSITIONS.astype(np.int8), n),
-            "median": pred[keep, 0, :].reshape(-1).astype(np.float32),
-            "hdpi_lower": pred[keep, 1, :].reshape(-1).astype(np.float32),
-            "hdpi_upper": pred[keep, 2, :].reshape(-1).astype(np.float32),
+            "median": np.ascontiguousarray(kp[:, 0, :], dtype=np.float32).reshape(-1),
+            "hdpi_lower": np.ascontiguousarray(kp[:, 1, :], dtype=np.float32).reshape(-1),
+            "hdpi_upper": np.ascontiguousarray(kp[:, 2, :], dtype=np.float32).reshape(-1),
             "shortname": _const_category(cfg.shortname, n * _lib.NPOS),
         },
         copy=False,
@@ -358,7 +418,7 @@ def prepare_fits(df_counts, cfg):
     file's fit); None when this rank's fit cache is a hit (get_fits decides)."""
     if _cache_hit(cfg):
         return None
-    return pack_counts(get_top_max_fits(df_counts, cfg.N_fits), cfg)
+    return pack_counts(get_top_max_fits(df_counts, cfg.N_fits), cfg, pinned=True)
 
 
 def get_fits(df_counts, cfg, opts=None, shard=True, writer=None, packed=None, deferred=False):
