@@ -141,8 +141,9 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.mdfit_hpdi68.restype = ctypes.c_int
     lib.mdfit_peak_probe.argtypes = [i64, i32, vp, vp]
     lib.mdfit_peak_probe.restype = ctypes.c_int
-    lib.mdfit_nuts_peak_probe.argtypes = [i64, i32, vp, vp]
-    lib.mdfit_nuts_peak_probe.restype = ctypes.c_int
+    if hasattr(lib, "mdfit_nuts_peak_probe"):  # (absent from round-3 builds loaded by tools/ for A/B)
+        lib.mdfit_nuts_peak_probe.argtypes = [i64, i32, vp, vp]
+        lib.mdfit_nuts_peak_probe.restype = ctypes.c_int
     lib.mdfit_objective.argtypes = [vp, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp]
     lib.mdfit_objective.restype = ctypes.c_int
     lib.mdfit_last_error.argtypes = []
