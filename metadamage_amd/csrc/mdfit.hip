@@ -1032,6 +1032,36 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
 // be seen), waits until every reserved slot is written (its writer is
 // resident, one store away) and drains the deferred items after the main
 // claim counter.  The late launch never waits on the fit.
+// An early HPDI wave hands its pending items to the defer list (see
+// hpdi_stream_kernel): true when they were taken (the wave then claims no
+// more), false when the late launch has closed the list already (every entry
+// is published then: keep waiting).  Out of line: the stream kernel is
+// register-bound, and this rarely-run path should not shape its allocation.
+__device__ __noinline__ bool defer_items(int* ws, int* defer, bool pending, int item) {
+  const int lane = (int)threadIdx.x;
+  const unsigned long long pm = __ballot(pending);
+  int base = -1;
+  if (lane == 0) {
+    int old = __hip_atomic_load(ws + kWsDefRes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (!(old & (int)kDefClosed)) {
+      if (__hip_atomic_compare_exchange_strong(ws + kWsDefRes, &old, old + __popcll(pm), __ATOMIC_RELAXED,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        base = old;
+        break;
+      }
+    }
+  }
+  base = __shfl(base, 0);
+  if (base < 0) return false;
+  if (pending) {
+    __hip_atomic_store(defer + base + __popcll(pm & ((1ull << lane) - 1ull)), item, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(ws + kWsDefDone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (lane == 0) __hip_atomic_store(ws + kWsEarlyQuit, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
 #ifndef MDFIT_STREAM_WAVES_PER_CU
 #define MDFIT_STREAM_WAVES_PER_CU 4  // A/B at 10k and 125k taxa (tools/overlap_exp.py): 4 with the fit waves' base priority 1
 #endif
@@ -1187,27 +1217,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
         if (!keep && (now - t_wait > defer_ticks ||
                       (now - t_wait > defer_ticks / 8 &&
                        __hip_atomic_load(ws + kWsEarlyQuit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0))) {
-          const unsigned long long pm = __ballot(pending);
-          int base = -1;
-          if (lane == 0) {
-            int old = __hip_atomic_load(ws + kWsDefRes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            while (!(old & (int)kDefClosed)) {
-              if (__hip_atomic_compare_exchange_strong(ws + kWsDefRes, &old, old + __popcll(pm), __ATOMIC_RELAXED,
-                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                base = old;
-                break;
-              }
-            }
-          }
-          base = __shfl(base, 0);
-          if (base >= 0) {
-            if (pending) {
-              __hip_atomic_store(defer + base + __popcll(pm & ((1ull << lane) - 1ull)), (int)item, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-              __hip_atomic_fetch_add(ws + kWsDefDone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-              pending = false;
-            }
-            if (lane == 0) __hip_atomic_store(ws + kWsEarlyQuit, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (defer_items(ws, defer, pending, (int)item)) {
+            pending = false;
             stop = true;
           } else {
             keep = true;  // the late launch runs: fit_kernel is done, every entry is published

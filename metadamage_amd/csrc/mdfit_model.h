@@ -209,12 +209,12 @@ __device__ __forceinline__ double point_contrib(const PointData& pd, const Theta
   const double a = D * phi, b = omD * phi;
   // paired so that each pair's lnGamma / psi / psi1 difference is formed as
   // soon as both halves exist (fewer live registers)
-  const LG3 t1 = lg3(pd.y + a);
-  const LG3 t4 = lg3(a);
+  const LG3 t1 = lg3<true, MDFIT_TLOG_FIT>(pd.y + a);
+  const LG3 t4 = lg3<true, MDFIT_TLOG_FIT>(a);
   const double la = t1.l - t4.l, Pa = t1.p - t4.p, Qa = t1.q - t4.q;
   double mag = fabs(t1.l) + fabs(t4.l);
-  const LG3 t2 = lg3(pd.N - pd.y + b);
-  const LG3 t5 = lg3(b);
+  const LG3 t2 = lg3<true, MDFIT_TLOG_FIT>(pd.N - pd.y + b);
+  const LG3 t5 = lg3<true, MDFIT_TLOG_FIT>(b);
   const double lb = t2.l - t5.l, Pb = t2.p - t5.p, Qb = t2.q - t5.q;
   mag += fabs(t2.l) + fabs(t5.l);
   const double lS = t3.l - t6.l, S = t6.p - t3.p, S1 = t6.q - t3.q;
@@ -260,14 +260,14 @@ __device__ __forceinline__ double point_contrib(const PointData& pd, const Theta
 template <bool kRowPhi = false>
 __device__ __forceinline__ double point_accum(const PointData& pd, const Theta& th,
                                               double acc[kNAcc], int accf = 0) {
-  const LG3 t3 = lg3(pd.N + th.phi);
+  const LG3 t3 = lg3<true, MDFIT_TLOG_FIT>(pd.N + th.phi);
   LG3 t6;
   if (kRowPhi) {
     t6.l = rowb<15>(t3.l);
     t6.p = rowb<15>(t3.p);
     t6.q = rowb<15>(t3.q);
   } else {
-    t6 = lg3(th.phi);
+    t6 = lg3<true, MDFIT_TLOG_FIT>(th.phi);
   }
   return point_contrib(pd, th, t3, t6, acc, accf);
 }

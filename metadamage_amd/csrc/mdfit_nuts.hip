@@ -196,13 +196,13 @@ __device__ __forceinline__ Pot potential(const PointData& pd, const double v[4],
   }
   const bool bad_lane = (pd.valid && !(D < 1.0)) || (pmd && A + c >= 1.0);
   const double a = D * phi, b = (1.0 - D) * phi;
-  const LG3 t1 = lg3<false>(pd.y + a);
-  const LG3 t4 = lg3<false>(a);
+  const LG3 t1 = lg3<false, MDFIT_TLOG_NUTS>(pd.y + a);
+  const LG3 t4 = lg3<false, MDFIT_TLOG_NUTS>(a);
   const double la = t1.l - t4.l, Pa = t1.p - t4.p;
-  const LG3 t2 = lg3<false>(pd.N - pd.y + b);
-  const LG3 t5 = lg3<false>(b);
+  const LG3 t2 = lg3<false, MDFIT_TLOG_NUTS>(pd.N - pd.y + b);
+  const LG3 t5 = lg3<false, MDFIT_TLOG_NUTS>(b);
   const double lb = t2.l - t5.l, Pb = t2.p - t5.p;
-  const LG3 t3 = lg3<false>(pd.N + phi);
+  const LG3 t3 = lg3<false, MDFIT_TLOG_NUTS>(pd.N + phi);
   const double t6l = rowb<15>(t3.l), t6p = rowb<15>(t3.p);  // pad lane: lg(0 + phi)
   const double ell = (la + lb) - (t3.l - t6l);
   const double lD = phi * (Pa - Pb);
@@ -265,7 +265,7 @@ __device__ __forceinline__ Pot potential2(const PointData pt[2], const double v[
   if (pmd) lprior += prA + prc;
 
   // the pad's lnGamma(0 + phi) pair: lane 7 (pair, forward half) or lane 15
-  const LG3 t3b = lg3<false>(pt[1].N + phi);
+  const LG3 t3b = lg3<false, MDFIT_TLOG_NUTS>(pt[1].N + phi);
   const bool src15 = whole || hi8;
   const double t6l = src15 ? rowb<15>(t3b.l) : rowb<7>(t3b.l);
   const double t6p = src15 ? rowb<15>(t3b.p) : rowb<7>(t3b.p);
@@ -290,13 +290,13 @@ __device__ __forceinline__ Pot potential2(const PointData pt[2], const double v[
     }
     bad_lane = bad_lane || (pd.valid && !(D < 1.0));
     const double a = D * phi, b = (1.0 - D) * phi;
-    const LG3 t1 = lg3<false>(pd.y + a);
-    const LG3 t4 = lg3<false>(a);
+    const LG3 t1 = lg3<false, MDFIT_TLOG_NUTS>(pd.y + a);
+    const LG3 t4 = lg3<false, MDFIT_TLOG_NUTS>(a);
     const double la = t1.l - t4.l, Pa = t1.p - t4.p;
-    const LG3 t2 = lg3<false>(pd.N - pd.y + b);
-    const LG3 t5 = lg3<false>(b);
+    const LG3 t2 = lg3<false, MDFIT_TLOG_NUTS>(pd.N - pd.y + b);
+    const LG3 t5 = lg3<false, MDFIT_TLOG_NUTS>(b);
     const double lb = t2.l - t5.l, Pb = t2.p - t5.p;
-    const LG3 t3 = pi == 1 ? t3b : lg3<false>(pd.N + phi);
+    const LG3 t3 = pi == 1 ? t3b : lg3<false, MDFIT_TLOG_NUTS>(pd.N + phi);
     const double ell = (la + lb) - (t3.l - t6l);
     const double lD = phi * (Pa - Pb);
     const double lF = D * Pa + (1.0 - D) * Pb + (t6p - t3.p);
@@ -1147,11 +1147,11 @@ __device__ __forceinline__ PotC potential_cd(const PointData pt[PPL], double x, 
   double t6l, t6p;
   LG3 t3b;
   if constexpr (PPL == 1) {
-    t3b = lg3<false>(pt[0].N + phi);
+    t3b = lg3<false, MDFIT_TLOG_NUTS>(pt[0].N + phi);
     t6l = rowb<15>(t3b.l);  // pad lane: lg(0 + phi)
     t6p = rowb<15>(t3b.p);
   } else {
-    t3b = lg3<false>(pt[1].N + phi);
+    t3b = lg3<false, MDFIT_TLOG_NUTS>(pt[1].N + phi);
     const bool src15 = whole || hi8;
     t6l = src15 ? rowb<15>(t3b.l) : rowb<7>(t3b.l);
     t6p = src15 ? rowb<15>(t3b.p) : rowb<7>(t3b.p);
@@ -1172,13 +1172,13 @@ __device__ __forceinline__ PotC potential_cd(const PointData pt[PPL], double x, 
     }
     bad_lane = bad_lane || (pd.valid && !(D < 1.0));
     const double a = D * phi, b = (1.0 - D) * phi;
-    const LG3 t1 = lg3<false>(pd.y + a);
-    const LG3 t4 = lg3<false>(a);
+    const LG3 t1 = lg3<false, MDFIT_TLOG_NUTS>(pd.y + a);
+    const LG3 t4 = lg3<false, MDFIT_TLOG_NUTS>(a);
     const double la = t1.l - t4.l, Pa = t1.p - t4.p;
-    const LG3 t2 = lg3<false>(pd.N - pd.y + b);
-    const LG3 t5 = lg3<false>(b);
+    const LG3 t2 = lg3<false, MDFIT_TLOG_NUTS>(pd.N - pd.y + b);
+    const LG3 t5 = lg3<false, MDFIT_TLOG_NUTS>(b);
     const double lb = t2.l - t5.l, Pb = t2.p - t5.p;
-    const LG3 t3 = (PPL == 1 || pi == 1) ? t3b : lg3<false>(pd.N + phi);
+    const LG3 t3 = (PPL == 1 || pi == 1) ? t3b : lg3<false, MDFIT_TLOG_NUTS>(pd.N + phi);
     const double ell = (la + lb) - (t3.l - t6l);
     const double lD = phi * (Pa - Pb);
     const double lF = D * Pa + (1.0 - D) * Pb + (t6p - t3.p);
@@ -2019,14 +2019,14 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
     for (int col = lo; col < hi; ++col) {
       const double yy = s_y[col], nn = s_N[col];
       const int k = col < kNHalf ? col : col - kNHalf;
-      const double lc = lg3<false>(nn + 1.0).l - lg3<false>(yy + 1.0).l - lg3<false>(nn - yy + 1.0).l;
+      const double lc = lg3<false, MDFIT_TLOG_NUTS>(nn + 1.0).l - lg3<false, MDFIT_TLOG_NUTS>(yy + 1.0).l - lg3<false, MDFIT_TLOG_NUTS>(nn - yy + 1.0).l;
       double mx = -INFINITY, sm = 0.0;
       for (int x = lane; x < S; x += kWave) {
         const double* th = smp + ((int64_t)s * S + x) * 4;
         const double D = d_at(th, pmd, k), phi = th[3];
         const double a = D * phi, b = (1.0 - D) * phi;
-        const double lp = lc + (lg3<false>(yy + a).l - lg3<false>(a).l) + (lg3<false>(nn - yy + b).l - lg3<false>(b).l) -
-                          (lg3<false>(nn + phi).l - lg3<false>(a + b).l);
+        const double lp = lc + (lg3<false, MDFIT_TLOG_NUTS>(yy + a).l - lg3<false, MDFIT_TLOG_NUTS>(a).l) + (lg3<false, MDFIT_TLOG_NUTS>(nn - yy + b).l - lg3<false, MDFIT_TLOG_NUTS>(b).l) -
+                          (lg3<false, MDFIT_TLOG_NUTS>(nn + phi).l - lg3<false, MDFIT_TLOG_NUTS>(a + b).l);
         s_v[x] = lp;
         mx = fmax(mx, lp);
         sm += lp;

@@ -58,25 +58,27 @@ __device__ __forceinline__ double flog(double x) {
   return normal ? r : (x == 0.0 ? -INFINITY : (x == INFINITY ? x : NAN));
 }
 
-#ifndef MDFIT_TLOG
-#define MDFIT_TLOG 0  // (off: A/B pending)
+#ifndef MDFIT_TLOG_FIT
+#define MDFIT_TLOG_FIT 0  // the fit kernel's point evaluation (A/B pending)
 #endif
-#if MDFIT_TLOG
+#ifndef MDFIT_TLOG_NUTS
+#define MDFIT_TLOG_NUTS 0  // the sampler's potential (A/B pending)
+#endif
 }  // namespace mdfit
 #include "mdfit_logtab.h"
 namespace mdfit {
 // Natural log by table (the lnGamma family's logs: arguments >= 10, and the
-// shift products), <= ~1 ulp for x away from 1: x = 2^e m, m in [1, 2), j =
-// the top 8 mantissa bits, c_j = 1 + (2j+1)/512 the centre of its interval
-// (mdfit_logtab.h: 1/c_j, c_j, ln c_j as hi + lo); r = (m - c_j) / c_j with
+// shift products), ~1 ulp for x away from 1: x = 2^e m, m in [1, 2), j = the
+// top 8 mantissa bits, c_j = 1 + (2j+1)/512 the centre of its interval
+// (mdfit_logtab.h: 1/c_j and ln c_j, one 16-B load); r = (m - c_j) / c_j with
 // m - c_j exact and |r| <= 2^-9, ln(1 + r) by a degree-6 polynomial
-// (truncation < 2^-66):
-//   ln x = (e ln2_hi + ln c_j hi) + (r + r^2 q(r) + e ln2_lo + ln c_j lo).
-// ~20 VALU + two 16-B table loads against flog's ~44 (its reciprocal, the
-// degree-7 reduction, the special cases).  NOT for x near 1 where ln x ~ 0
-// (absolute, not relative, accuracy there): flog1p keeps flog.  Inputs:
-// finite and > 0 normal; kZero also 0 (-> -inf) and subnormals (pre-scaled)
-// -- lnGamma's shift product, which is 0 at a = 0.
+// (truncation < 2^-66):  ln x = (e ln2_hi + ln c_j) + (r + r^2 q(r) + e ln2_lo).
+// (ln c_j rounded to a double: <= 5.6e-17 absolute, a quarter ulp of ln x for
+// x >= 10.)  ~20 VALU + one table load against flog's ~44 (its reciprocal,
+// the degree-7 reduction, the special cases).  NOT for x near 1 where
+// ln x ~ 0 (absolute, not relative, accuracy there): flog1p keeps flog.
+// Inputs: finite and > 0 normal; kZero also 0 (-> -inf) and subnormals
+// (pre-scaled) -- lnGamma's shift product, which is 0 at a = 0.
 template <bool kZero = false>
 __device__ __forceinline__ double flog_t(double x) {
   constexpr double kLn2Hi = 6.93147180369123816490e-01;
@@ -92,24 +94,19 @@ __device__ __forceinline__ double flog_t(double x) {
   const int e = (int)(hw >> 20) - eoff;
   const int j = (int)((hw >> 12) & 255u);
   const double m = __hiloint2double((int)((hw & 0x000FFFFFu) | 0x3FF00000u), __double2loint(xn));
-  const double2 ic = *reinterpret_cast<const double2*>(&g_logtab[j][0]);  // (1/c, c)
-  const double2 lc = *reinterpret_cast<const double2*>(&g_logtab[j][2]);  // ln c (hi, lo)
-  const double r = (m - ic.y) * ic.x;
+  const double2 t = *reinterpret_cast<const double2*>(&g_logtab[j][0]);  // (1/c, ln c)
+  const double c = fma((double)(2 * j + 1), 1.0 / 512.0, 1.0);             // exact
+  const double r = (m - c) * t.x;
   const double r2 = r * r;
   double q = fma(r, -1.0 / 6.0, 1.0 / 5.0);
   q = fma(r, q, -0.25);
   q = fma(r, q, 1.0 / 3.0);
   q = fma(r, q, -0.5);
   const double de = (double)e;
-  const double hi = fma(de, kLn2Hi, lc.x);
-  const double lo = fma(de, kLn2Lo, lc.y);
-  const double y = hi + (r + fma(r2, q, lo));
+  const double hi = fma(de, kLn2Hi, t.y);
+  const double y = hi + (r + fma(r2, q, de * kLn2Lo));
   return kZero ? (x > 0.0 ? y : -INFINITY) : y;
 }
-#else
-template <bool kZero = false>
-__device__ __forceinline__ double flog_t(double x) { return flog(x); }
-#endif
 
 // log(1 + x), x > -1: Goldberg's correction log(u) * x / (u - 1), u = 1 + x.
 __device__ __forceinline__ double flog1p(double x) {
@@ -150,8 +147,11 @@ struct LG3 {
   double q;  // trigamma(x)
 };
 
-// kTri = false: lnGamma and psi only (the sampler needs no Hessian)
-template <bool kTri = true>
+// kTri = false: lnGamma and psi only (the sampler needs no Hessian).
+// kTab: the logs by flog_t (the table) instead of flog -- the fit kernel's
+// point evaluation and the sampler's potential (MDFIT_TLOG_FIT / _NUTS); the
+// HPDI and record kernels keep flog (register-bound there).
+template <bool kTri = true, bool kTab = false>
 __device__ __forceinline__ LG3 lg3(double x) {
   constexpr double kHalfLog2Pi = 0.91893853320467274178;  // 0.5 ln(2 pi)
   double P = 1.0, dP = 0.0, d2P = 0.0;
@@ -172,7 +172,7 @@ __device__ __forceinline__ LG3 lg3(double x) {
 #ifdef MDFIT_DEV_FAKELOG  // development: timing bound of a cheaper log (WRONG results)
   const double lx = (double)__builtin_amdgcn_logf((float)xs) * 0.6931471805599453;
 #else
-  const double lx = flog_t(xs);
+  const double lx = kTab ? flog_t(xs) : flog(xs);
 #endif
   // lnGamma(xs) ~ (xs - 1/2) ln xs - xs + ln(2 pi)/2 + r (1/12 - r2 (1/360 - ...))
   double sl = fma(r2, -1.0 / 156.0, 691.0 / 360360.0);
@@ -207,7 +207,7 @@ __device__ __forceinline__ LG3 lg3(double x) {
 #ifdef MDFIT_DEV_FAKELOG
     L -= (double)__builtin_amdgcn_logf((float)P) * 0.6931471805599453;
 #else
-    L -= flog_t<true>(P);
+    L -= kTab ? flog_t<true>(P) : flog(P);
 #endif
     Ps -= s1;
     if (kTri) Q += s1 * s1 - d2P * iP;  // sum 1/(x+j)^2
