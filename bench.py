@@ -383,6 +383,9 @@ def main():
                 "point_evals_per_taxon": useful_pe / T,
             },
             "status_ok_frac": float((st == 0).mean()),
+            # items the HPDI stream's early waves handed to the late launch in the
+            # last call (their bounded wait): 0 when undisturbed
+            "hpdi_deferred_items": int(fb.workspace[128:132].view(torch.int32).item() & ~0x40000000),
         }
         if world == 1:
             line["host_to_host"] = host_to_host(engine, b, opts, dev, max(5, args.steps // 2))

@@ -1239,7 +1239,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
 __global__ void special_kernel(const double* __restrict__ x, int64_t n, double* __restrict__ o) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const LG3 r = lg3(x[i]);
+  const LG3 r = lg3<true, MDFIT_TLOG_FIT>(x[i]);  // (the fit kernel's form, the one its parity test covers)
   o[3 * i + 0] = r.l;
   o[3 * i + 1] = r.p;
   o[3 * i + 2] = r.q;

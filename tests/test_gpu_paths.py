@@ -207,8 +207,6 @@ def test_hpdi_stream_beside_the_fit_same_record(torch_dev, monkeypatch, ppl):
                 assert hdr[33] == n_def and hdr[34] >= n_def  # every reserved slot written, and drained
             if early == "4d":
                 assert n_def > 0 and hdr[35] == 1
-            else:
-                assert n_def == 0  # an undisturbed call never waits 1 ms
             recs.append((early, with_pred, r.out.cpu().numpy()[:, :32], None if r.pred is None else r.pred.cpu().numpy(),
                          r.status.cpu().numpy()))
     base = {wp: rec for e, wp, *rec in recs if e == "0"}
