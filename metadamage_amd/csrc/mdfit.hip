@@ -469,13 +469,13 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
     } else {
       // lg3(phi) from a pad: lane 15's point b (all-position: both halves;
       // pair: the reverse half), lane 7's point b (pair: the forward half)
-      const LG3 t3b = lg3(pb.N + th.phi);
+      const LG3 t3b = lg3<true, MDFIT_TLOG_FIT>(pb.N + th.phi);
       const bool src15 = whole || h == 1;
       LG3 t6;
       t6.l = src15 ? rowb<15>(t3b.l) : rowb<7>(t3b.l);
       t6.p = src15 ? rowb<15>(t3b.p) : rowb<7>(t3b.p);
       t6.q = src15 ? rowb<15>(t3b.q) : rowb<7>(t3b.q);
-      point_contrib(pa, th, lg3(pa.N + th.phi), t6, acc, accf);
+      point_contrib(pa, th, lg3<true, MDFIT_TLOG_FIT>(pa.N + th.phi), t6, acc, accf);
       double accb[kNAcc];
 #pragma unroll
       for (int j = 0; j < kNAcc; ++j) accb[j] = 0.0;

@@ -20,13 +20,26 @@
 
 namespace mdfit {
 
-// FP64 reciprocal: v_rcp_f64 + two Newton steps (faithful, no IEEE div sequence)
+// FP64 reciprocal: v_rcp_f64 + two Newton steps (faithful, no IEEE div sequence).
+// Measured on gfx950 (tools/micro/rcp_accuracy.hip, 2^28 log-uniform x):
+// v_rcp_f64 alone is off by up to 2.1e8 ulp (~2^-25), one Newton step 10 ulp,
+// two 0 (the correctly rounded 1/x).
 __device__ __forceinline__ double rcp(double x) {
   double r = __builtin_amdgcn_rcp(x);
   r = fma(fma(-x, r, 1.0), r, r);
   r = fma(fma(-x, r, 1.0), r, r);
   return r;
 }
+// One Newton step (<= 10 ulp): for reciprocals that only scale series
+// corrections (lnGamma's Stirling terms, the shift sums of psi), where the
+// relative error stays < 3e-15 of the function (MDFIT_RCP1, A/B).
+__device__ __forceinline__ double rcp1(double x) {
+  const double r = __builtin_amdgcn_rcp(x);
+  return fma(fma(-x, r, 1.0), r, r);
+}
+#ifndef MDFIT_RCP1
+#define MDFIT_RCP1 0
+#endif
 
 // Natural log, <= ~1 ulp (the classic reduction x = 2^e (1+f), 1+f in
 // [sqrt(1/2), sqrt(2)), log(1+f) = f - hfsq + s (hfsq + R(s^2)), s = f/(2+f),
@@ -167,7 +180,7 @@ __device__ __forceinline__ LG3 lg3(double x) {
     }
     xs = x + 10.0;
   }
-  const double r = rcp(xs);
+  const double r = MDFIT_RCP1 ? rcp1(xs) : rcp(xs);
   const double r2 = r * r;
 #ifdef MDFIT_DEV_FAKELOG  // development: timing bound of a cheaper log (WRONG results)
   const double lx = (double)__builtin_amdgcn_logf((float)xs) * 0.6931471805599453;
@@ -202,7 +215,7 @@ __device__ __forceinline__ LG3 lg3(double x) {
     Q = r + 0.5 * r2 + r * r2 * sq;
   }
   if (shift) {
-    const double iP = rcp(P);
+    const double iP = MDFIT_RCP1 ? rcp1(P) : rcp(P);
     const double s1 = dP * iP;          // sum 1/(x+j)
 #ifdef MDFIT_DEV_FAKELOG
     L -= (double)__builtin_amdgcn_logf((float)P) * 0.6931471805599453;
