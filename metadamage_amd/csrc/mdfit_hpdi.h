@@ -176,28 +176,15 @@ __device__ __forceinline__ void greedy_window(const Pmf& P, double& lo, double& 
   double M = P.pm;
   double pl = A > 0.0 ? P.pm * rcp(ratio(P, A - 1.0)) : 0.0;
   double pr = B < N ? P.pm * ratio(P, B) : 0.0;
-  // Each side's next two step factors, computed ahead (software pipelining):
-  // a step's probability update is one multiply by a factor that was ready
-  // a step or more earlier, so the ratio's reciprocals (~10 dependent FP64
-  // operations) leave the loop's critical path.  Same operations on the same
-  // values as the one-ahead form (a left step A -> A-1 multiplies by
-  // rcp(ratio(A-2)), a right step B -> B+1 by ratio(B+1)): bit-identical.
-  auto lfac = [&](double a) { return a - 1.0 > 0.0 ? rcp(ratio(P, a - 2.0)) : 0.0; };  // step a -> a-1
-  auto rfac = [&](double b) { return b + 1.0 < N ? ratio(P, b + 1.0) : 0.0; };      // step b -> b+1
-  double lq1 = lfac(A), lq2 = lfac(A - 1.0), rq1 = rfac(B), rq2 = rfac(B + 1.0);
   while (M < kMass && (pl > 0.0 || pr > 0.0)) {
     if (pl >= pr) {
       A -= 1.0;
       M += pl;
-      pl = A > 0.0 ? pl * lq1 : 0.0;
-      lq1 = lq2;
-      lq2 = lfac(A - 1.0);
+      pl = A > 0.0 ? pl * rcp(ratio(P, A - 1.0)) : 0.0;
     } else {
       B += 1.0;
       M += pr;
-      pr = B < N ? pr * rq1 : 0.0;
-      rq1 = rq2;
-      rq2 = rfac(B + 1.0);
+      pr = B < N ? pr * ratio(P, B) : 0.0;
     }
   }
   lo = A;

@@ -72,10 +72,10 @@ __device__ __forceinline__ double flog(double x) {
 }
 
 #ifndef MDFIT_TLOG_FIT
-#define MDFIT_TLOG_FIT 1  // the fit kernel's point evaluation: C2 1.238 -> 1.218 ms, 125k 9.94 -> 9.88 ms (A/B)
+#define MDFIT_TLOG_FIT 0  // the fit kernel's point evaluation: within +-1 % at C2 and 125k (A/B), so off
 #endif
 #ifndef MDFIT_TLOG_NUTS
-#define MDFIT_TLOG_NUTS 0  // the sampler's potential (A/B pending)
+#define MDFIT_TLOG_NUTS 1  // the sampler's potential and WAIC: C3 chain + post ~7.0 -> 6.3 s (A/B)
 #endif
 }  // namespace mdfit
 #include "mdfit_logtab.h"
