@@ -85,7 +85,7 @@ namespace mdfit {
 // top 8 mantissa bits, c_j = 1 + (2j+1)/512 the centre of its interval
 // (mdfit_logtab.h: 1/c_j and ln c_j, one 16-B load); r = (m - c_j) / c_j with
 // m - c_j exact and |r| <= 2^-9, ln(1 + r) by a degree-6 polynomial
-// (truncation < 2^-66):  ln x = (e ln2_hi + ln c_j) + (r + r^2 q(r) + e ln2_lo).
+// (truncation < 2^-66):  ln x = e ln2_hi + (ln c_j + (r + r^2 q(r) + e ln2_lo)).
 // (ln c_j rounded to a double: <= 5.6e-17 absolute, a quarter ulp of ln x for
 // x >= 10.)  ~20 VALU + one table load against flog's ~44 (its reciprocal,
 // the degree-7 reduction, the special cases).  NOT for x near 1 where
@@ -116,8 +116,9 @@ __device__ __forceinline__ double flog_t(double x) {
   q = fma(r, q, 1.0 / 3.0);
   q = fma(r, q, -0.5);
   const double de = (double)e;
-  const double hi = fma(de, kLn2Hi, t.y);
-  const double y = hi + (r + fma(r2, q, de * kLn2Lo));
+  // e ln2_hi is exact (ln2_hi has 21 trailing zero bits): one rounding at the
+  // end, as fdlibm's, instead of two (~0.5 ulp typical instead of ~1)
+  const double y = de * kLn2Hi + (t.y + (r + fma(r2, q, de * kLn2Lo)));
   return kZero ? (x > 0.0 ? y : -INFINITY) : y;
 }
 
