@@ -1117,7 +1117,10 @@ __device__ __forceinline__ PotC potential_cd(const PointData pt[PPL], double x, 
   const int c = (int)(threadIdx.x & 3);
   const bool hi8 = PPL == 2 && (threadIdx.x & 8);
   const double e = exp(c < 3 ? -fabs(x) : x);
-  const double sp = flog1p(e);
+  // ln(1 + e), e = exp(-|x|) in (0, 1]: it enters only the log prior, whose
+  // absolute (not relative) accuracy matters in U ~ 1e5..1e7, so the fast form
+  // takes the table log of the rounded 1 + e (absolute error <= 1.2e-16)
+  const double sp = MDFIT_TLOG_NUTS ? flog_t(1.0 + e) : flog1p(e);
   const double rr = rcp(1.0 + e);
   const bool pos = x >= 0.0;
   const double p = pos ? rr : e * rr, omp = pos ? e * rr : rr;
