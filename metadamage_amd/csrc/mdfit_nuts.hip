@@ -1103,6 +1103,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PPL == 1 
 #define MDFIT_NUTS_CD_WAVES 4  // 128 VGPRs, no spill with MachineLICM off (build_hip)
 #endif
 
+// ln(1 + e) of the multinomial weights' log-sum-exp, e = exp(-|w1 - w2|) in
+// [0, 1]: the log-weights enter only through exp differences, so absolute
+// accuracy is what counts, and the fast form takes the table log of the
+// rounded 1 + e (absolute error <= 1.2e-16; MDFIT_TLOG_NUTS)
+__device__ __forceinline__ double lae1p(double e) { return MDFIT_TLOG_NUTS ? flog_t(1.0 + e) : flog1p(e); }
+
 struct PotC {
   double U;
   double g;  // this lane's component of the gradient
@@ -1555,7 +1561,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       } else {
         const double m = fmax(s_w, w);
         const double e = exp(-fabs(s_w - w));
-        const double nw = m == -INFINITY ? -INFINITY : m + flog1p(e);
+        const double nw = m == -INFINITY ? -INFINITY : m + lae1p(e);
         const double prob = (w >= s_w ? 1.0 : e) * rcp(1.0 + e);
         if ((leaf_ctr >> 4) != ul_chunk) {  // next 16 leaf uniforms, 16 / kG per lane
 #pragma unroll
@@ -1642,7 +1648,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         }
         {
           const double m = fmax(C.t_w, s_w);
-          C.t_w = m == -INFINITY ? -INFINITY : m + flog1p(em);
+          C.t_w = m == -INFINITY ? -INFINITY : m + lae1p(em);
         }
         const double trs = V[kVtr][c] + srs;
         V[kVtr][c] = trs;
