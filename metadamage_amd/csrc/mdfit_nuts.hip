@@ -1357,6 +1357,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
     if (lane == 0) swin_n = n;
   }
   __syncthreads();
+#ifdef MDFIT_STAMP
+  // the sections of nuts_chain_kernel's split (see there)
+  constexpr int kNStamp = 10;
+  __shared__ unsigned long long sstamp[kNStamp];
+  unsigned long long acc_t[kNStamp] = {};
+  const unsigned long long t_begin = nstamp();
+  sstamp[0] = 0;
+#endif
 
   // hot chain state, row-uniform (the vectors: component c)
   int mode = 0, drained = 0, whole = 0, it = 0;
@@ -1376,6 +1384,33 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
 #endif
 
   while (true) {
+#ifdef MDFIT_STAMP
+    {
+      const unsigned long long now = nstamp();
+      if (sstamp[0] != 0) {
+        constexpr int order[9] = {0, 1, 2, 5, 6, 7, 8, 3, 4};
+        int cur = 0;
+        unsigned long long last = sstamp[0];
+#pragma unroll
+        for (int j = 1; j < 9; ++j) {
+          const int k = order[j];
+          if (sstamp[k] == 0) continue;
+          const unsigned long long d = sstamp[k] - last;
+#pragma unroll
+          for (int q = 0; q < 9; ++q)
+            if (q == cur) acc_t[q] += d;
+          last = sstamp[k];
+          cur = k;
+        }
+#pragma unroll
+        for (int q = 0; q < 9; ++q)
+          if (q == cur) acc_t[q] += now - last;
+        acc_t[9] += 1;
+      }
+      sstamp[0] = now;
+      for (int j = 1; j < kNStamp; ++j) sstamp[j] = 0;
+    }
+#endif
     // (-DMDFIT_CD_HOIST_LAYOUT, development: the layout of the prologue held
     // across the loop instead -- 33 VGPRs spilled at 4 waves/SIMD)
 #ifndef MDFIT_CD_HOIST_LAYOUT
@@ -1470,6 +1505,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       pd[p].pmd = pmdq;
     }
 
+    NSTAMP(1);
     // ---- 2. one evaluation: the initial point, or a leapfrog step ------------
     const double rh = rm - 0.5 * step * gr;
     const double zev = mode == kInit ? z : z + step * im * rh;
@@ -1484,6 +1520,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
 #else
     const PotC P = potential_cd<PPL>(pd, zev, whole);
 #endif
+    NSTAMP(2);
     if (!running) continue;
     const double rn = rh - 0.5 * step * P.g;
     z = zev;
@@ -1583,6 +1620,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       }
       s_div = dv;
       ++leaf_ctr;
+      NSTAMP(5);
       int imin, imax;
       ckpt_idxs(n_leaf, &imin, &imax);
       double srs4[4];
@@ -1628,6 +1666,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       rm = rn;
       gr = P.g;
       if (s_turn || s_div || n_leaf == nmax) {
+        NSTAMP(6);
         // merge the subtree into the tree: biased progressive sampling
         const double em = exp(-fabs(C.t_w - s_w));
         const double prob = (s_turn || s_div) ? 0.0 : (s_w > C.t_w ? 1.0 : em);
@@ -1658,6 +1697,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         C.t_n += s_n;
         ++C.t_depth;
         if (C.t_depth >= kMaxDepth || t_turn || t_div) {
+          NSTAMP(7);
           // ---- the transition is complete: adapt or keep the draw ----------
           const double accp = C.t_acc / (double)C.t_n;
           if (it < W) {
@@ -1721,6 +1761,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
             begin_iter = true;
           }
         } else {
+          NSTAMP(8);
           // next doubling
           const int j = C.t_depth;
           if (j == 8) {  // the draws of depths 8 and 9 (entries 8, 9 of the caches)
@@ -1743,6 +1784,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       }  // (else: the next leaf of the subtree continues from (z, r, g) with the same step)
     }
 
+    NSTAMP(3);
     if (begin_find) {
       // one probe of find_reasonable_step_size from the current state
       if (mode != kFind || C.f_m == 0) {
@@ -1802,7 +1844,15 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       nmax = 1;
       step = right ? C.eps : -C.eps;
     }
+    NSTAMP(4);
   }
+#ifdef MDFIT_STAMP
+  if (lane == 0 && g_nuts_stamp) {
+    unsigned long long* w = g_nuts_stamp + 16 * (size_t)blockIdx.x;
+    for (int j = 0; j < kNStamp; ++j) w[j] = acc_t[j];
+    w[10] = nstamp() - t_begin;
+  }
+#endif
 #ifndef MDFIT_NO_UTIL
   if (threadIdx.x == 0) {
     atomicAdd(reinterpret_cast<unsigned long long*>(ws + 32), util_trips);
