@@ -917,14 +917,14 @@ __global__ __launch_bounds__(kWave) void assemble_kernel(
 // -> only z = +1, the D_max_{lower,upper}_hpdi columns) or plain arrays
 // (mdfit_hpdi68, parity tests).
 // ---------------------------------------------------------------------------
-// one K4a item's pmf: N, alpha, beta, its output index (kFit: taxon * per +
-// position), skip = no window (N = 0, or the fit failed)
 template <bool kFit>
-__device__ __forceinline__ void hpdi_item(const HpdiIO& io, int64_t item, bool valid, double& N, double& a, double& b,
-                                          int64_t& oitem, bool& skip) {
-  N = a = b = 0.0;
-  skip = true;
-  oitem = item;
+__global__ __launch_bounds__(kWave) void hpdi_prep_kernel(HpdiIO io, int64_t n_items, int* __restrict__ ctr,
+                                                          hpdi::WideRec* __restrict__ recs) {
+  const int64_t item = (int64_t)blockIdx.x * kWave + threadIdx.x;
+  const bool valid = item < n_items;
+  double N = 0.0, a = 0.0, b = 0.0;
+  bool skip = true;
+  int64_t oitem = item;  // the output index (kFit: taxon * per + position)
   if (valid) {
     if (kFit) {
       // items in ready-list order: entry item / per, stream-ordered after the
@@ -952,142 +952,7 @@ __device__ __forceinline__ void hpdi_item(const HpdiIO& io, int64_t item, bool v
       skip = !(N > 0.0);
     }
   }
-}
-
-template <bool kFit>
-__global__ __launch_bounds__(kWave) void hpdi_prep_kernel(HpdiIO io, int64_t n_items, int* __restrict__ ctr,
-                                                          hpdi::WideRec* __restrict__ recs) {
-  const int64_t item = (int64_t)blockIdx.x * kWave + threadIdx.x;
-  const bool valid = item < n_items;
-  double N, a, b;
-  int64_t oitem;
-  bool skip;
-  hpdi_item<kFit>(io, item, valid, N, a, b, oitem, skip);
   hpdi_position<kFit>(io, oitem, valid, skip, N, a, b, n_items, ctr, recs);
-}
-
-// K4a with the greedy walks sorted by length (the product form), two launches:
-// hpdi_sort_kernel -- a block of kSortBlock items classifies them (lane = item,
-// as hpdi_prep_kernel: degenerate windows written, wide ones appended to K4b's
-// list) and counting-sorts its narrow windows by key (~sd, mdfit_hpdi.h) into
-// its segment of the narrow list (the greedy's inputs, structure of arrays);
-// hpdi_greedy_kernel -- one lane per list slot walks them in that order, so the
-// 64 walks of a wave have similar lengths.  (A wave runs as long as its longest
-// walk: in item order the lanes of a wave idle ~70 % of the greedy's steps at
-// 125k taxa, sorted per 1024 items about half as many steps are issued.  The
-// walks are a separate launch of one-wave blocks: walked inside the sorting
-// block, its longest wave held the block's slot on the CU.)  Same window per
-// item, whatever the order.
-struct NarrowList {
-  double *N, *a, *b, *m, *pm;
-  int64_t* item;  // the output index
-  int* count;     // per block: its segment's length
-};
-constexpr int kSortBlock = 1024;
-__host__ __device__ constexpr int64_t narrow_list_bytes(int64_t n_items) {
-  return n_items * (5 * (int64_t)sizeof(double) + (int64_t)sizeof(int64_t)) +
-         ((n_items + kSortBlock - 1) / kSortBlock) * (int64_t)sizeof(int) + 64;
-}
-inline NarrowList narrow_list(void* mem, int64_t n_items) {
-  char* p = static_cast<char*>(mem);
-  NarrowList l;
-  l.N = reinterpret_cast<double*>(p);
-  l.a = l.N + n_items;
-  l.b = l.a + n_items;
-  l.m = l.b + n_items;
-  l.pm = l.m + n_items;
-  l.item = reinterpret_cast<int64_t*>(l.pm + n_items);
-  l.count = reinterpret_cast<int*>(l.item + n_items);
-  return l;
-}
-
-template <bool kFit>
-__global__ __launch_bounds__(kSortBlock) void hpdi_sort_kernel(HpdiIO io, int64_t n_items, int* __restrict__ ctr,
-                                                               hpdi::WideRec* __restrict__ recs, NarrowList nl) {
-  __shared__ int shist[hpdi::kNarrowKeys], sbase[hpdi::kNarrowKeys + 1];
-  const int tid = (int)threadIdx.x, lane = tid & (kWave - 1);
-  if (tid < hpdi::kNarrowKeys) shist[tid] = 0;
-  __syncthreads();
-  const int64_t item = (int64_t)blockIdx.x * kSortBlock + tid;
-  const bool valid = item < n_items;
-  double N, a, b;
-  int64_t oitem;
-  bool skip;
-  hpdi_item<kFit>(io, item, valid, N, a, b, oitem, skip);
-  int key = -1;
-  hpdi::NarrowRec nr;
-  hpdi::WideRec rec;
-  bool wide = false;
-  if (valid) {
-    double lo = NAN, hi = NAN;
-    const int cls = skip ? hpdi::kDone : hpdi::classify_position(N, a, b, lo, hi, nr, key, rec);
-    wide = cls == hpdi::kWide;
-    if (cls == hpdi::kDone) hpdi_write<kFit>(io, oitem, N, lo, hi);
-    if (cls != hpdi::kNarrow) key = -1;
-  }
-  // the wide windows: appended as hpdi_position does (per wave)
-  bool near = false;
-  if (wide) {
-    const double tau = sqrt(rec.sd * rec.sd + (rec.mu - rec.m) * (rec.mu - rec.m));
-    near = rec.m < 1.5 * tau || rec.N - rec.m < 1.5 * tau;
-  }
-  const unsigned long long mf = __ballot(wide && near), mb = __ballot(wide && !near);
-  if ((mf | mb) != 0ull) {
-    int bf = 0, bb = 0;
-    if (lane == 0) {
-      if (mf) bf = atomicAdd(ctr, __popcll(mf));
-      if (mb) bb = atomicAdd(ctr + 2, __popcll(mb));
-    }
-    bf = __shfl(bf, 0);
-    bb = __shfl(bb, 0);
-    if (wide) {
-      rec.item = oitem;
-      const unsigned long long below = (1ull << lane) - 1ull;
-      const int64_t slot = near ? (int64_t)(bf + __popcll(mf & below)) : n_items - 1 - (bb + __popcll(mb & below));
-      recs[slot] = rec;
-    }
-  }
-  // counting sort of the narrow windows by key (the order inside a key is the
-  // LDS atomics' -- any order gives the same windows)
-  const int rank = key >= 0 ? atomicAdd(&shist[key], 1) : 0;
-  __syncthreads();
-  if (tid < kWave) {  // exclusive scan of the kNarrowKeys (= 64) counts by one wave
-    static_assert(hpdi::kNarrowKeys == kWave, "one key per lane of the scanning wave");
-    const int c = shist[tid];
-    int x = c;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-      const int y = __shfl_up(x, o, kWave);
-      if (tid >= o) x += y;
-    }
-    sbase[tid] = x - c;
-    if (tid == kWave - 1) {
-      sbase[kWave] = x;
-      nl.count[blockIdx.x] = x;
-    }
-  }
-  __syncthreads();
-  if (key >= 0) {
-    const int64_t j = (int64_t)blockIdx.x * kSortBlock + sbase[key] + rank;
-    nl.N[j] = nr.N;
-    nl.a[j] = nr.a;
-    nl.b[j] = nr.b;
-    nl.m[j] = nr.m;
-    nl.pm[j] = nr.pm;
-    nl.item[j] = oitem;
-  }
-}
-
-template <bool kFit>
-__global__ __launch_bounds__(kWave) void hpdi_greedy_kernel(HpdiIO io, int64_t n_items, NarrowList nl) {
-  const int64_t j = (int64_t)blockIdx.x * kWave + threadIdx.x;
-  const int64_t blk = (int64_t)blockIdx.x / (kSortBlock / kWave);
-  const int n = nl.count[blk];  // (one load per wave)
-  if ((int)(j - blk * kSortBlock) >= n || j >= n_items) return;
-  const hpdi::NarrowRec w{nl.N[j], nl.a[j], nl.b[j], nl.m[j], nl.pm[j]};
-  double lo, hi;
-  hpdi::greedy_narrow(w, lo, hi);
-  hpdi_write<kFit>(io, nl.item[j], w.N, lo, hi);
 }
 
 // one lane per wide window at a time: every trip each busy lane runs one level
@@ -1625,25 +1490,13 @@ struct ForkScope {
 
 // K4a (unless the fit kernel did its work: prep = false) and K4b
 template <bool kFit>
-int launch_hpdi(const mdfit::HpdiIO& io, int64_t n_items, int* ctr, mdfit::hpdi::WideRec* recs, void* narrow_mem,
-                hipStream_t s, bool prep = true) {
+int launch_hpdi(const mdfit::HpdiIO& io, int64_t n_items, int* ctr, mdfit::hpdi::WideRec* recs, hipStream_t s,
+                bool prep = true) {
   if (n_items == 0) return 0;
   if (prep) {
-    // (MDFIT_HPDI_SORTED=1: the greedy walks sorted by length, under evaluation)
-    if (env_int("MDFIT_HPDI_SORTED", 0) != 0) {
-      const mdfit::NarrowList nl = mdfit::narrow_list(narrow_mem, n_items);
-      const unsigned gs = (unsigned)((n_items + mdfit::kSortBlock - 1) / mdfit::kSortBlock);
-      hipLaunchKernelGGL(mdfit::hpdi_sort_kernel<kFit>, dim3(gs), dim3(mdfit::kSortBlock), 0, s, io, n_items, ctr, recs,
-                         nl);
-      if (int rc = check_launch("hpdi_sort_kernel")) return rc;
-      hipLaunchKernelGGL(mdfit::hpdi_greedy_kernel<kFit>, dim3(gs * (unsigned)(mdfit::kSortBlock / mdfit::kWave)),
-                         dim3(mdfit::kWave), 0, s, io, n_items, nl);
-      if (int rc = check_launch("hpdi_greedy_kernel")) return rc;
-    } else {
-      hipLaunchKernelGGL(mdfit::hpdi_prep_kernel<kFit>, dim3((unsigned)((n_items + mdfit::kWave - 1) / mdfit::kWave)),
-                         dim3(mdfit::kWave), 0, s, io, n_items, ctr, recs);
-      if (int rc = check_launch("hpdi_prep_kernel")) return rc;
-    }
+    hipLaunchKernelGGL(mdfit::hpdi_prep_kernel<kFit>, dim3((unsigned)((n_items + mdfit::kWave - 1) / mdfit::kWave)),
+                       dim3(mdfit::kWave), 0, s, io, n_items, ctr, recs);
+    if (int rc = check_launch("hpdi_prep_kernel")) return rc;
   }
   // no more waves than are resident, and no more than the items need (the
   // kernel strides over the wide list, whose length only the device knows)
@@ -1713,12 +1566,8 @@ int64_t mdfit_workspace_bytes(int64_t n_taxa, const mdfit_opts* opts) {
   // PMD-all modes (48 B per taxon); from kStreamMaxTaxa taxa (the HPDI after
   // the fit, K4a -> K4b) room for every position's wide-window record
   // (+ the HPDI stream's defer list at the end)
-  // (and K4a's sorted list of narrow windows)
-  const int64_t n_pos = n_taxa * mdfit::kNPos;
   return 256 + n_taxa * mdfit::kReadyStride * (int64_t)sizeof(double) +
-         (n_taxa >= kStreamMaxTaxa
-              ? n_pos * (int64_t)sizeof(mdfit::hpdi::WideRec) + mdfit::narrow_list_bytes(n_pos)
-              : 0) +
+         (n_taxa >= kStreamMaxTaxa ? n_taxa * mdfit::kNPos * (int64_t)sizeof(mdfit::hpdi::WideRec) : 0) +
          defer_cap(n_taxa) * (int64_t)sizeof(int);
 }
 
@@ -1833,8 +1682,7 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
     io.out = out;
     io.pred = pred;
     io.per = per;
-    mdfit::hpdi::WideRec* recs = hpdi_recs_after_ready(workspace, n_taxa);
-    if (int rc = launch_hpdi<true>(io, n_items, ws + mdfit::kHpdiCtr, recs, recs + n_taxa * mdfit::kNPos, s))
+    if (int rc = launch_hpdi<true>(io, n_items, ws + mdfit::kHpdiCtr, hpdi_recs_after_ready(workspace, n_taxa), s))
       return rc;
   }
   if (int rc = fork_as.join()) return rc;
@@ -1871,7 +1719,7 @@ int mdfit_hpdi68(const double* N, const double* alpha, const double* beta, int64
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)hip_stream;
   void* ws = nullptr;
-  const size_t bytes = 256 + (size_t)n * sizeof(mdfit::hpdi::WideRec) + (size_t)mdfit::narrow_list_bytes(n);
+  const size_t bytes = 256 + (size_t)n * sizeof(mdfit::hpdi::WideRec);
   if (hipMallocAsync(&ws, bytes, s) != hipSuccess) return set_err(MDFIT_E_HIP, "hipMallocAsync");
   if (hipMemsetAsync(ws, 0, 256, s) != hipSuccess) return set_err(MDFIT_E_HIP, "hipMemsetAsync");
   mdfit::HpdiIO io{};
@@ -1880,7 +1728,7 @@ int mdfit_hpdi68(const double* N, const double* alpha, const double* beta, int64
   io.b = beta;
   io.lo = lo;
   io.hi = hi;
-  int rc = launch_hpdi<false>(io, n, static_cast<int*>(ws) + mdfit::kHpdiCtr, hpdi_recs(ws), hpdi_recs(ws) + n, s);
+  int rc = launch_hpdi<false>(io, n, static_cast<int*>(ws) + mdfit::kHpdiCtr, hpdi_recs(ws), s);
   (void)hipFreeAsync(ws, s);
   return rc;
 }

@@ -206,26 +206,16 @@ __device__ __forceinline__ void set_pmf(Pmf& P, double N, double a, double b, do
   P.pm = pm;
 }
 
-// the greedy's inputs for one narrow window, and its sort key (K4a sorts a
-// block's narrow windows by key so the lanes of a wave walk similar lengths:
-// the walk is ~2 sd points, sd <= kSigGreedy; 0 when the mode alone holds 0.68)
-struct NarrowRec {
-  double N, a, b, m, pm;
-};
-constexpr int kNarrowKeys = 64;
-
-// window of one position: kDone (lo, hi set: a degenerate pmf), kNarrow (the
-// greedy's inputs in nr, its sort key in key), kWide (rec filled)
-enum { kDone = 0, kNarrow = 1, kWide = 2 };
-__device__ __forceinline__ int classify_position(double N, double a, double b, double& lo, double& hi,
-                                                 NarrowRec& nr, int& key, WideRec& rec) {
+// window of one position: returns true when done here (lo, hi set), false
+// when it is wide (rec filled)
+__device__ __forceinline__ bool prep_position(double N, double a, double b, double& lo, double& hi, WideRec& rec) {
   if (!(a > 0.0)) {
     lo = hi = 0.0;
-    return kDone;
+    return true;
   }
   if (!(b > 0.0)) {
     lo = hi = N;
-    return kDone;
+    return true;
   }
   const double phi = a + b;
   double m = ceil(((a - 1.0) * N - (b - 1.0)) / (phi - 2.0));
@@ -233,13 +223,10 @@ __device__ __forceinline__ int classify_position(double N, double a, double b, d
   const double pm = exp(bb_logpmf_ab(m, N, a, b, phi));
   const double sd = sqrt(N * a * b * (phi + N) / (phi * phi * (phi + 1.0)));
   if (sd <= kSigGreedy || pm >= kMass) {
-    nr.N = N;
-    nr.a = a;
-    nr.b = b;
-    nr.m = m;
-    nr.pm = pm;
-    key = pm >= kMass ? 0 : min(kNarrowKeys - 1, (int)(sd * (kNarrowKeys / kSigGreedy)));
-    return kNarrow;
+    Pmf P;
+    set_pmf(P, N, a, b, m, pm);
+    greedy_window(P, lo, hi);
+    return true;
   }
   rec.N = N;
   rec.a = a;
@@ -256,23 +243,7 @@ __device__ __forceinline__ int classify_position(double N, double a, double b, d
     rec.iz[j] = A.iz;
     rec.c[j] = A.c;
   }
-  return kWide;
-}
-
-__device__ __forceinline__ void greedy_narrow(const NarrowRec& nr, double& lo, double& hi) {
-  Pmf P;
-  set_pmf(P, nr.N, nr.a, nr.b, nr.m, nr.pm);
-  greedy_window(P, lo, hi);
-}
-
-// window of one position: returns true when done here (lo, hi set; the greedy
-// run inline when narrow), false when it is wide (rec filled)
-__device__ __forceinline__ bool prep_position(double N, double a, double b, double& lo, double& hi, WideRec& rec) {
-  NarrowRec nr;
-  int key;
-  const int cls = classify_position(N, a, b, lo, hi, nr, key, rec);
-  if (cls == kNarrow) greedy_narrow(nr, lo, hi);
-  return cls != kWide;
+  return false;
 }
 
 // ---------------------------------------------------------------------------

@@ -256,43 +256,3 @@ def test_two_calls_on_two_streams_at_once(torch_dev):
             assert np.array_equal(r.status.cpu().numpy(), ref.status.cpu().numpy()), (rep, T)
             hdr = r.workspace[:256].view(torch.int32).cpu().numpy()
             assert hdr[8] == T and hdr[11] == 0
-
-
-def test_sorted_greedy_walks_same_windows(torch_dev, monkeypatch):
-    """K4a sorts each block's greedy walks by length before walking them (the
-    product); against the walks in item order (MDFIT_HPDI_SORTED=0) every window
-    is the same: through the array entry point on a wide (N, alpha, beta) mix,
-    degenerate items included, and through a 60k-taxon fit (K4a / K4b after the
-    fit kernel)."""
-    torch = torch_dev
-    from metadamage_amd import _lib, engine
-    from metadamage_amd.synthetic import generate
-
-    rng = np.random.default_rng(7)
-    n = 150_000
-    N = np.floor(10 ** rng.uniform(0, 7, n))
-    D = rng.uniform(0.0, 0.6, n)
-    phi = 10 ** rng.uniform(0.5, 4, n)
-    a, b = D * phi, (1 - D) * phi
-    N[::97] = 0.0
-    a[::89] = 0.0
-    b[::83] = 0.0
-    got = {}
-    for flag in ("1", "0"):
-        monkeypatch.setenv("MDFIT_HPDI_SORTED", flag)
-        got[flag] = engine.hpdi68(N, a, b)
-    for x, y in zip(got["1"], got["0"]):
-        assert np.array_equal(x, y, equal_nan=True)
-
-    T = _lib.STREAM_MAX_TAXA
-    bt = generate(T, seed=5)
-    ty, tN, tm = engine.to_device_counts(bt.y, bt.N, bt.mm)
-    opts = _lib.default_opts()
-    recs = {}
-    for flag in ("1", "0"):
-        monkeypatch.setenv("MDFIT_HPDI_SORTED", flag)
-        r = engine.fit_batch_device(ty, tN, tm, opts)
-        torch.cuda.synchronize()
-        recs[flag] = (r.out[:, :_lib.NRESULT].cpu().numpy(), r.pred.cpu().numpy(), r.status.cpu().numpy())
-    for x, y in zip(recs["1"], recs["0"]):
-        assert np.array_equal(x, y, equal_nan=True)
