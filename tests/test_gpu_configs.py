@@ -71,7 +71,12 @@ def test_c3_nuts_100k(engine, oracle_lib):
     torch.cuda.synchronize()
     out, st = res.out.cpu().numpy(), res.status.cpu().numpy()
     assert (st == 0).all(), np.flatnonzero(st != 0)[:10]  # every taxon OK (as in every box run so far)
-    assert np.isfinite(out[st == 0][:, [0, 1, 4, 5, 6, 15, 18, 21]]).all()
+    cols = [0, 1, 4, 5, 6, 15, 18, 21]
+    bad = np.flatnonzero(~np.isfinite(out[:, cols]).all(1))
+    # (one box run of round 4 saw a non-finite column here, not reproduced in
+    # the runs after it: name the taxa, fields and sub-fit diagnostics if it recurs)
+    assert bad.size == 0, [(int(t), [_lib.RESULT_FIELDS[c] for c in cols if not np.isfinite(out[t, c])],
+                            out[t, :25].tolist(), out[t, _lib.F_DIAG:].tolist()) for t in bad[:3]]
     sub = 30_000 + np.arange(64)  # a contiguous subsample (one oracle call, index_base keyed)
     smp = engine.samples_view(res, T, opts)[torch.as_tensor(sub, device=res.out.device)].cpu().numpy()
     del res

@@ -1,5 +1,8 @@
 """Time mdfit_fit_batch of several builds of the engine on the same batch
-(development tool: kernel-design A/B at the bench workload).
+(development tool: kernel-design A/B at the bench workload).  Each library has
+its own side streams; at batches where the HPDI streams beside the fit (C2) a
+library loaded second runs ~3.5 % slower whatever its code (the streams share
+hardware queues): A/B those one library per process (tools/overlap_exp.py --lib).
 
     python tools/variant_bench.py metadamage_amd/libmdfit_A.so metadamage_amd/libmdfit_B.so
 """
