@@ -2126,8 +2126,11 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
     const double mdr = wsum(dr) / kNHalf;
     const double varr = wsum(vf * (dr - mdr) * (dr - mdr)) / kNHalf;
     const double nsr = (wsum(vf * s_waic[5][pr_]) - wsum(vf * s_waic[3][pr_])) / sqrt(kNHalf * varr);
-    // asymmetry: PMD-all vs concat(PMD-fwd, PMD-rev)
-    const double fr = lane < kNHalf ? s_waic[2][p] : s_waic[3][p];
+    // asymmetry: PMD-all vs concat(PMD-fwd, PMD-rev).  Lanes >= 30 (v30 = 0) read
+    // a written entry: s_waic[3][0..14] is never written (the reverse fit has
+    // points 15..29 only), and 0 * a stale LDS NaN there made the sums NaN --
+    // whenever the kernel before on that CU had left one (round 4)
+    const double fr = lane < kNHalf ? s_waic[2][p] : s_waic[3][lane < kNPos ? p : kNHalf];
     const double dc = v30 * (dP - fr);
     const double mdc = wsum(dc) / kNPos;
     const double varc = wsum(v30 * (dc - mdc) * (dc - mdc)) / kNPos;
