@@ -185,6 +185,15 @@ int mdfit_betabinom_logpmf(const double* y, const double* N, const double* alpha
 int mdfit_special(const double* x, int64_t n, double* out3, void* hip_stream);
 
 /*
+ * Test helper: fills every CU's LDS with NaN (one launch of blocks holding the
+ * largest LDS a block may take, several per CU), so that a kernel launched after
+ * it on the stream that reads LDS it did not write sees NaN there.  The library's
+ * kernels never do; tests/test_gpu_paths.py checks that records are bit-identical
+ * after a poisoning.
+ */
+int mdfit_poison_lds(void* hip_stream);
+
+/*
  * MAP predictive HPDI (MDFIT-HPDI v1): the 68 % highest-
  * probability window [lo, hi] (integer counts, returned as double) of
  * BetaBinomial(alpha, beta, N), the population form of numpyro's

@@ -70,6 +70,7 @@ EXPORTED_SYMBOLS = [
     "mdfit_hpdi68",
     "mdfit_peak_probe",
     "mdfit_nuts_peak_probe",
+    "mdfit_poison_lds",
     "mdfit_objective",
     "mdfit_nuts_potential",
     "mdfit_profile_enable",
@@ -141,6 +142,9 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
     lib.mdfit_hpdi68.restype = ctypes.c_int
     lib.mdfit_peak_probe.argtypes = [i64, i32, vp, vp]
     lib.mdfit_peak_probe.restype = ctypes.c_int
+    if hasattr(lib, "mdfit_poison_lds"):
+        lib.mdfit_poison_lds.argtypes = [vp]
+        lib.mdfit_poison_lds.restype = ctypes.c_int
     if hasattr(lib, "mdfit_nuts_peak_probe"):  # (absent from round-3 builds loaded by tools/ for A/B)
         lib.mdfit_nuts_peak_probe.argtypes = [i64, i32, vp, vp]
         lib.mdfit_nuts_peak_probe.restype = ctypes.c_int

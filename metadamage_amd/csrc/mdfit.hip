@@ -30,6 +30,7 @@
 // idle.)  Everything is FP64 (the reference enables x64, fits.py:32).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -1291,6 +1292,13 @@ __global__ void betabinom_kernel(const double* __restrict__ y, const double* __r
   }
 }
 
+// mdfit_poison_lds: NaN into the whole dynamic LDS of the block
+__global__ __launch_bounds__(1024) void poison_lds_kernel(int n_doubles) {
+  extern __shared__ double s_poison[];
+  for (int i = (int)threadIdx.x; i < n_doubles; i += (int)blockDim.x) s_poison[i] = __longlong_as_double(0x7FF8DEAD0BADF00Dll);
+  __syncthreads();
+}
+
 // Register-only throughput probe of the fit kernel's point evaluation
 // (make_theta + point_accum<kRowPhi>, the row layout of fit_kernel: lane 15 of
 // every row a pad): each wave evaluates `iters` times 60 points on a
@@ -1523,6 +1531,7 @@ int launch_hpdi(const mdfit::HpdiIO& io, int64_t n_items, int* ctr, mdfit::hpdi:
                 bool prep = true) {
   if (n_items == 0) return 0;
   if (prep) {
+    mdfit::host::debug_poison(s);
     hipLaunchKernelGGL(mdfit::hpdi_prep_kernel<kFit>, dim3((unsigned)((n_items + mdfit::kWave - 1) / mdfit::kWave)),
                        dim3(mdfit::kWave), 0, s, io, n_items, ctr, recs);
     if (int rc = check_launch("hpdi_prep_kernel")) return rc;
@@ -1530,6 +1539,7 @@ int launch_hpdi(const mdfit::HpdiIO& io, int64_t n_items, int* ctr, mdfit::hpdi:
   // no more waves than are resident, and no more than the items need (the
   // kernel strides over the wide list, whose length only the device knows)
   const int64_t g = fit_grid(mdfit::hpdi_wide_kernel<kFit>, n_items, mdfit::kWave, env_int("MDFIT_HPDI_WAVES_PER_CU", 0));
+  mdfit::host::debug_poison(s);
   hipLaunchKernelGGL(mdfit::hpdi_wide_kernel<kFit>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, io, n_items, ctr,
                      recs);
   return check_launch("hpdi_wide_kernel");
@@ -1663,6 +1673,7 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   if (early_per_cu > 0) {
     const int64_t g = std::min<int64_t>(fit_grid(mdfit::hpdi_stream_kernel<true>, n_items, mdfit::kWave, early_per_cu),
                                         kDeferCap / mdfit::kWave);
+    mdfit::host::debug_poison(fork_hp.side());
     hipLaunchKernelGGL(mdfit::hpdi_stream_kernel<true>, dim3((unsigned)g), dim3(mdfit::kWave), 0, fork_hp.side(), N,
                        n_taxa, per, out, pred, ws, (const double*)ready, defer, defer_ticks);
     if (int rc = check_launch("hpdi_stream_kernel")) return rc;
@@ -1695,12 +1706,14 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   // one left); they write disjoint fields of the record and join before the
   // call returns
   ForkScope fork_as(fk, s, 1);
+  mdfit::host::debug_poison(fork_as.side());
   hipLaunchKernelGGL(mdfit::assemble_kernel, dim3((unsigned)n_taxa), dim3(mdfit::kWave), 0, fork_as.side(), y, N,
                      mm, n_taxa, out, pred, status);
   if (int rc = check_launch("assemble_kernel")) return rc;
   if (stream) {
     const int64_t g = fit_grid(mdfit::hpdi_stream_kernel<false>, n_items, mdfit::kWave,
                                env_int("MDFIT_HPDI_WAVES_PER_CU", 0));
+    mdfit::host::debug_poison(s);
     hipLaunchKernelGGL(mdfit::hpdi_stream_kernel<false>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, N, n_taxa, per,
                        out, pred, ws, (const double*)ready, defer, defer_ticks);
     if (int rc = check_launch("hpdi_stream_kernel")) return rc;
@@ -1770,6 +1783,29 @@ int mdfit_special(const double* x, int64_t n, double* out3, void* hip_stream) {
                      x, n, out3);
   return check_launch("special_kernel");
 }
+
+int mdfit_poison_lds(void* hip_stream) {
+  int dev = 0, n_cu = 256, lds_block = 65536, lds_cu = 163840;
+  if (hipGetDevice(&dev) != hipSuccess) return set_err(MDFIT_E_HIP, "hipGetDevice");
+  (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipDeviceGetAttribute(&lds_block, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
+  (void)hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev);
+  lds_block = std::max(1024, std::min(lds_block, lds_cu));
+  const int per_cu = std::max(1, lds_cu / lds_block);
+  // several rounds of blocks per CU: every CU gets blocks whatever the dispatch order
+  hipLaunchKernelGGL(mdfit::poison_lds_kernel, dim3((unsigned)(4 * n_cu * per_cu)), dim3(1024), (size_t)lds_block,
+                     (hipStream_t)hip_stream, lds_block / (int)sizeof(double));
+  return check_launch("poison_lds_kernel");
+}
+
+}  // extern "C" (reopened below)
+
+void mdfit::host::debug_poison(hipStream_t s) {
+  const char* e = std::getenv("MDFIT_DEBUG_POISON_LDS");
+  if (e != nullptr && std::atoi(e) != 0) (void)mdfit_poison_lds(s);
+}
+
+extern "C" {
 
 int mdfit_peak_probe(int64_t n_waves, int32_t iters, double* sink, void* hip_stream) {
   if (n_waves <= 0 || iters <= 0 || !sink) return set_err(MDFIT_E_ARG, "bad arguments");

@@ -58,6 +58,12 @@ int64_t fit_grid(K kernel, int64_t ntask, int fits_per_wave, int cap_per_cu = 0,
 }
 }  // namespace mdfit::host
 
+namespace mdfit::host {
+// MDFIT_DEBUG_POISON_LDS=1 (tests): NaN into every CU's LDS on stream s
+// (mdfit_poison_lds) -- called before each LDS-using kernel of a call
+void debug_poison(hipStream_t s);
+}  // namespace mdfit::host
+
 namespace mdfit::nuts {
 // sampling mode (mdfit_nuts.hip): workspace = 256 B of queue counters, then
 // the chains' samples double[T][6][num_samples][4] = (q, A, c, phi)

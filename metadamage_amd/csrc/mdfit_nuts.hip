@@ -2335,11 +2335,13 @@ int fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t 
   auto chain = MDFIT_NUTS_CD ? nuts_chain_cd<kPPL> : nuts_chain_kernel<kPPL>;
   const int64_t g = host::fit_grid(chain, 4 * n_taxa, kPPL == 1 ? 2 : 4, 0, force ? std::atoi(force) : 0);
   host::prof_mark(1, s);
+  host::debug_poison(s);
   hipLaunchKernelGGL(chain, dim3((unsigned)g), dim3(kWave), 0, s, y, N, n_taxa, o, out, ws, samples);
   if (int rc = host::check_launch("nuts_chain_kernel")) return rc;
   host::prof_mark(2, s);
   size_t sv_bytes = sizeof(double);
   while (sv_bytes < (size_t)o.num_samples * sizeof(double)) sv_bytes <<= 1;  // lds_sort pads to 2^k
+  host::debug_poison(s);
   hipLaunchKernelGGL(nuts_post_kernel, dim3((unsigned)n_taxa), dim3(kWave), sv_bytes, s, y, N, mm, n_taxa, o,
                      samples, out, pred, status);
   return host::check_launch("nuts_post_kernel");

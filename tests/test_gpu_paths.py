@@ -256,3 +256,32 @@ def test_two_calls_on_two_streams_at_once(torch_dev):
             assert np.array_equal(r.status.cpu().numpy(), ref.status.cpu().numpy()), (rep, T)
             hdr = r.workspace[:256].view(torch.int32).cpu().numpy()
             assert hdr[8] == T and hdr[11] == 0
+
+
+@pytest.mark.parametrize("mode,T", [("map", 1_500), ("map", 60_000), ("nuts", 96)])
+def test_poisoned_lds_same_record(torch_dev, monkeypatch, mode, T):
+    """No kernel of a call reads LDS it did not write: with every CU's LDS set to
+    NaN before each LDS-using kernel (MDFIT_DEBUG_POISON_LDS, mdfit_poison_lds),
+    the record, predictions and statuses are those of a call without -- the MAP
+    streamed path, the MAP K4a / K4b path (from 60k taxa) and the sampler.  (Round
+    4: the sampler's asymmetry read one unwritten LDS entry at weight 0, and a
+    stale NaN there made the column NaN.)"""
+    torch = torch_dev
+    from metadamage_amd import _lib, engine
+    from metadamage_amd.synthetic import generate
+
+    b = generate(T, seed=26)
+    ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm)
+    opts = _lib.default_opts(mode=_lib.MODE_NUTS if mode == "nuts" else _lib.MODE_MAP)
+    if mode == "nuts":
+        opts.num_warmup, opts.num_samples = 60, 80
+    recs = []
+    for poison in ("0", "1"):
+        monkeypatch.setenv("MDFIT_DEBUG_POISON_LDS", poison)
+        r = engine.fit_batch_device(ty, tN, tm, opts)
+        torch.cuda.synchronize()
+        recs.append((r.out.cpu().numpy(), r.pred.cpu().numpy(), r.status.cpu().numpy()))
+    for x, y in zip(*recs):
+        assert np.array_equal(x, y, equal_nan=True)
+    if mode == "nuts":  # (the columns test_c3_nuts_100k checks)
+        assert np.isfinite(recs[1][0][recs[1][2] == 0][:, [0, 1, 4, 5, 6, 15, 18, 21]]).all()
