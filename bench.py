@@ -13,9 +13,17 @@ predictive HPDI.  One step = one mdfit_fit_batch launch with inputs resident in
 HBM.
 
 N > 1 (configs[3], C4): 1,000,000 TaxIDs in total, strong scaling: rank r fits
-its contiguous 1M/N shard (synthetic, seed 3 + 1000 r) and every step ends with
-the ONE RCCL gather of the packed result records to rank 0 (synchronous, inside
-the timed region; no step overlaps another).
+its contiguous 1M/N shard and every step ends with the ONE RCCL gather of the
+packed result records to rank 0 (synchronous, inside the timed region; no step
+overlaps another).  Global taxon i of C4 is row i % 125,000 of C4's synthetic
+per-GPU share (seed 3): every rank's shard and the one-GPU base (c4_one_gpu)
+fit exactly the same taxa, so value_N / (N * c4_one_gpu) is an exact
+efficiency.
+
+The N = 1 line also carries c3_nuts: BASELINE config C3 (100k TaxIDs, the
+reference's own inference -- NUTS 500 warmup + 1000 draws on all 6 sub-fits,
+fits.py:382-387, 792-799), one warm-up and one timed call, with its rooflines
+and its distributional parity against the CPU oracle's sampler.
 
 Printed JSON (rank 0): the driver contract fields plus
   roofline          HBM roofline of the dominant kernel (fit_kernel): SURVEY.md
@@ -51,6 +59,8 @@ sys.path.insert(0, str(ROOT))
 
 TAXA_PER_GPU = 10_000
 C4_TAXA = 1_000_000
+C4_SHARE = C4_TAXA // 8  # C4's per-GPU share at N = 8 (seed 3): the rows every C4 shard is cut from
+C3_TAXA = 100_000
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # bytes per taxon:
 #  algorithmic: y,N 2x30x4 in + 26 numeric result fields x8 out
@@ -76,6 +86,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c4-base", action="store_true",
                     help="N=1: skip the C4-on-one-GPU strong-scaling base (c4_one_gpu)")
+    ap.add_argument("--no-c3", action="store_true", help="N=1 MAP: skip the C3 NUTS leg (c3_nuts)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the process's core share (affinity, OMP_NUM_THREADS)")
     ap.add_argument("--workload", choices=["c2", "c4"], default=None,
                     help="default: c2 at N = 1 (the headline), c4 (1M taxa, strong scaling) at N > 1")
@@ -101,18 +112,38 @@ def pmc_traffic(kernel: str = "fit_kernel", taxa: int = TAXA_PER_GPU):
         return None
 
 
-def c4_one_gpu(engine, _lib, generate, dev, stream, steps: int = 3, warmup: int = 1) -> dict:
-    """The strong-scaling base of the N>1 lines: C4's 1M TaxIDs fitted on ONE GPU
-    in one call, inputs resident in HBM.  1M synthetic taxa take ~1 min to
-    generate on the host, so C4's rank-0 share (125k, seed 3) is tiled 8x on
-    the device -- the same per-taxon work distribution."""
+def c4_rows(rank: int, world: int, total: int = C4_TAXA, share: int = C4_SHARE):
+    """C4's taxa of `rank`: its contiguous shard [lo, hi) of the `total`
+    global taxa, and the rows of the synthetic share they are (global taxon i
+    = share row i % share; 1M distinct synthetic taxa take ~1 min to generate
+    on the host, the share a few seconds).  Every world size fits the same
+    global taxa, so the N > 1 lines and c4_one_gpu divide like for like."""
+    from metadamage_amd.distributed import shard_range
+
+    lo, hi = shard_range(total, rank, world)
+    return lo, hi, np.arange(lo, hi, dtype=np.int64) % share
+
+
+def c4_counts(engine, generate, rows, dev):
+    """Device y, N, mm of C4's rows (the share, seed 3, copied to the device
+    once and gathered there)."""
     import torch
 
-    share, reps = C4_TAXA // 8, 8
-    b = generate(share, seed=3)
-    ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm, device=dev)
-    ty, tN, tm = (x.repeat((reps,) + (1,) * (x.dim() - 1)).contiguous() for x in (ty, tN, tm))
-    T = share * reps
+    b = generate(C4_SHARE, seed=3)
+    sy, sN, sm = engine.to_device_counts(b.y, b.N, b.mm, device=dev)
+    idx = torch.as_tensor(rows, device=dev)
+    return tuple(x.index_select(0, idx).contiguous() for x in (sy, sN, sm))
+
+
+def c4_one_gpu(engine, _lib, generate, dev, stream, steps: int = 3, warmup: int = 1) -> dict:
+    """The strong-scaling base of the N>1 lines: C4's 1M TaxIDs fitted on ONE GPU
+    in one call, inputs resident in HBM -- the taxa of every N > 1 line's
+    shards together (c4_rows)."""
+    import torch
+
+    _, _, rows = c4_rows(0, 1)
+    ty, tN, tm = c4_counts(engine, generate, rows, dev)
+    T = rows.size
     opts = _lib.default_opts(mode=_lib.MODE_MAP)
     fb = engine.alloc_outputs(T, device=dev, opts=opts)
     for _ in range(warmup):
@@ -134,7 +165,8 @@ def c4_one_gpu(engine, _lib, generate, dev, stream, steps: int = 3, warmup: int 
         "steps": steps,
         "warmup": warmup,
         "status_ok_frac": ok,
-        "data": f"C4's rank-0 share ({share} synthetic TaxIDs, seed 3) tiled {reps}x on the device",
+        "data": f"C4's 1M TaxIDs: global taxon i = row i % {C4_SHARE} of the synthetic share (seed 3), as in "
+        "the N > 1 shards",
         "note": "the strong-scaling base for the N>1 lines (C4: 1M TaxIDs, 1M/N per rank + one gather): "
         "efficiency_N = value_N / (N * this value)",
     }
@@ -206,13 +238,15 @@ def main():
 
     # ---- synthetic shard, resident in HBM before timing -------------------
     if workload == "c4":
-        lo, hi = shard_range(C4_TAXA, rank, world)
-        T, cap, seed, total_per_step = hi - lo, shard_capacity(C4_TAXA, world), 3 + 1000 * rank, C4_TAXA
+        lo, hi, rows = c4_rows(rank, world)
+        T, cap, total_per_step = hi - lo, shard_capacity(C4_TAXA, world), C4_TAXA
+        ty, tN, tm = c4_counts(engine, generate, rows, dev)
+        b = None
     else:
-        T = args.taxa or (100_000 if nuts else TAXA_PER_GPU)
+        T = args.taxa or (C3_TAXA if nuts else TAXA_PER_GPU)
         lo, cap, seed, total_per_step = rank * T, T, (2 if nuts else 1) + rank, T * world
-    b = generate(T, seed=seed)  # C2 seed 1, C3 seed 2, C4 seed 3
-    ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm, device=dev)
+        b = generate(T, seed=seed)  # C2 seed 1, C3 seed 2, C4 seed 3
+        ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm, device=dev)
     rec = alloc_records(cap, dev)
     fb = engine.FitBatch(rec.out[:T], rec.pred[:T], rec.status[:T])
     opts = _lib.default_opts(mode=_lib.MODE_NUTS if nuts else _lib.MODE_MAP, index_base=lo)
@@ -287,15 +321,7 @@ def main():
         # at byte 128 / 136): wave-trips with a running slot, running slot-trips
         util = fb.workspace[128:144].view(torch.int64).cpu().numpy()
         # compute roofline: register-only probe of the same potential evaluation
-        n_waves, iters = 256 * 20, 32
-        engine.peak_probe(n_waves, iters, stream=stream, nuts=True)  # warm
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(3):
-            engine.peak_probe(n_waves, iters, stream=stream, nuts=True)
-        e1.record(stream)
-        torch.cuda.synchronize(dev)
-        probe_rate = 3 * n_waves * 60 * iters / (e0.elapsed_time(e1) / 1e3)  # 60 points per wave-iteration
+        probe_rate = nuts_probe_rate(engine, dev, stream)
         print(json.dumps(nuts_line(args, T, world, elapsed, call_ms_sum, fit_ms_sum, n_calls, o, st, b, smp,
                                    util, probe_rate)), flush=True)
     elif rank == 0:
@@ -339,8 +365,9 @@ def main():
             "scaling": "strong" if workload == "c4" else "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (SURVEY.md §8(d) generator; " + ("C4 seed 3 + 1000 x rank per shard)" if workload == "c4"
-                                                                    else "C2 seed 1 + rank)"),
+            "data": "synthetic (SURVEY.md §8(d) generator; " + (
+                f"C4: global taxon i = row i % {C4_SHARE} of the seed-3 share, rank r its contiguous 1M/N shard)"
+                if workload == "c4" else "C2 seed 1 + rank)"),
             "config": {
                 "workload": wl,
                 "taxa_total": total_per_step,
@@ -387,10 +414,17 @@ def main():
             # last call (their bounded wait): 0 when undisturbed
             "hpdi_deferred_items": int(fb.workspace[128:132].view(torch.int32).item() & ~0x40000000),
         }
-        if world == 1:
+        if world == 1 and b is not None:
             line["host_to_host"] = host_to_host(engine, b, opts, dev, max(5, args.steps // 2))
         if ranks is not None:
+            from metadamage_amd.distributed import REC_BYTES
+
             line["per_rank"] = ranks
+            # what the one gather moves into rank 0 per step: every peer's
+            # padded shard of 564-B records (25 result doubles, 90 prediction
+            # floats, the status)
+            line["gather_bytes_to_rank0"] = REC_BYTES * cap * (world - 1)
+            line["gather_record_bytes"] = REC_BYTES
             line["per_rank_note"] = ("a step split into the fit call and the one gather by the wall clock, "
                                      "measured after the timed region (synchronised per phase)")
         if (world == 1 and workload == "c2" or workload == "c4" and world > 1) and not args.no_c4_base:
@@ -398,7 +432,12 @@ def main():
             # (at N > 1 the other ranks wait at the closing barrier):
             # value_N / (N * c4_one_gpu.value) is the C4 scaling efficiency
             line["c4_one_gpu"] = c4_one_gpu(engine, _lib, generate, dev, stream)
-        if not args.no_cpu_baseline and world == 1:  # the CPU baseline is an N=1 figure
+        if world == 1 and workload == "c2" and not args.no_c3:
+            # config C3, the reference's own inference, in the driver's default run
+            del fb, rec
+            torch.cuda.empty_cache()
+            line["c3_nuts"] = c3_nuts(engine, _lib, generate, dev, stream, args)
+        if not args.no_cpu_baseline and world == 1 and b is not None:  # the CPU baseline is an N=1 figure
             line["cpu_baseline"], ref = cpu_baseline(b, cores, visible)
             if ref_dispatch is not None:
                 line["cpu_baseline"]["reference_dispatch"] = ref_dispatch
@@ -407,6 +446,61 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def nuts_probe_rate(engine, dev, stream) -> float:
+    """Point evaluations/s of nuts_probe_kernel, the register-only loop over the
+    sampler's potential at the chain kernel's occupancy (the compute ceiling)."""
+    import torch
+
+    n_waves, iters = 256 * 20, 32
+    engine.peak_probe(n_waves, iters, stream=stream, nuts=True)  # warm
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(3):
+        engine.peak_probe(n_waves, iters, stream=stream, nuts=True)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    return 3 * n_waves * 60 * iters / (e0.elapsed_time(e1) / 1e3)  # 60 points per wave-iteration
+
+
+def c3_nuts(engine, _lib, generate, dev, stream, args) -> dict:
+    """BASELINE config C3 inside the default N = 1 run: 100k synthetic TaxIDs
+    (seed 2), NUTS 500 warmup + 1000 draws on all 6 sub-fits (the reference's
+    inference, fits.py:382-387, 792-799), one warm-up and one timed call
+    (inputs resident in HBM, HIP events on the launch stream around the chain
+    kernel), with nuts_line's rooflines, CPU baseline and 64-taxon
+    distributional parity."""
+    import types
+
+    import torch
+
+    T = C3_TAXA
+    b = generate(T, seed=2)
+    ty, tN, tm = engine.to_device_counts(b.y, b.N, b.mm, device=dev)
+    opts = _lib.default_opts(mode=_lib.MODE_NUTS)
+    fb = engine.alloc_outputs(T, device=dev, opts=opts)
+    engine.fit_batch_device(ty, tN, tm, opts, fb, stream=stream)  # warm-up call
+    torch.cuda.synchronize(dev)
+    engine.profile_enable(True, fit_only=True)
+    t0 = time.perf_counter()
+    engine.fit_batch_device(ty, tN, tm, opts, fb, stream=stream)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    _, fit_ms_sum, n_calls = engine.profile_read()
+    engine.profile_enable(False)
+    o = fb.out.cpu().numpy()
+    st = fb.status.cpu().numpy()
+    smp = engine.samples_view(fb, T, opts)[:64].cpu().numpy()
+    util = fb.workspace[128:144].view(torch.int64).cpu().numpy()
+    del fb, ty, tN, tm
+    torch.cuda.empty_cache()
+    probe_rate = nuts_probe_rate(engine, dev, stream)
+    a = types.SimpleNamespace(steps=1, warmup=1, no_cpu_baseline=args.no_cpu_baseline, cpu_threads=args.cpu_threads)
+    line = nuts_line(a, T, 1, elapsed, elapsed * 1e3, fit_ms_sum, n_calls, o, st, b, smp, util, probe_rate)
+    for k in ("metric", "higher_is_better", "vs_baseline", "n_gpus"):
+        line.pop(k, None)
+    return line
 
 
 def host_to_host(engine, b, opts, dev, steps: int) -> dict:

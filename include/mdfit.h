@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MDFIT_ABI_VERSION 1
+#define MDFIT_ABI_VERSION 2
 
 /* Dense count layout: one row of MDFIT_LD uint32 per taxon.
  * Column i < 15 is forward position z = i+1 (y = CT, N = C by default);
@@ -146,8 +146,12 @@ void mdfit_default_opts(mdfit_opts* opts);
  *               return path, so the call stays ordered on hip_stream and
  *               capturable in a graph.  MAP below 60k taxa: the predictive
  *               HPDI kernel runs beside the fit kernel and waits for modes
- *               the fit kernel's waves publish (release / acquire); the two
- *               grids are sized to be co-resident on an otherwise idle device.
+ *               the fit kernel's waves publish (relaxed, order-free: each
+ *               field of a ready-list entry is written once as the bit
+ *               complement of its value into a list the call zeroed, and an
+ *               entry is taken when every field reads non-zero -- no fence,
+ *               DESIGN.md §4); the two grids are sized to be co-resident on
+ *               an otherwise idle device.
  *               The waits are bounded: a wave that makes no progress for 1 ms
  *               hands its items to the HPDI launch after the fit and exits, so
  *               concurrent calls or other kernels on the device (e.g. an RCCL

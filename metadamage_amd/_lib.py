@@ -15,7 +15,7 @@ PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = PKG_DIR / "libmdfit.so"
 
 # mirrors of include/mdfit.h
-ABI_VERSION = 1
+ABI_VERSION = 2
 NPOS = 30
 NHALF = 15
 LD = 32

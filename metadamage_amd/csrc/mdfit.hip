@@ -85,6 +85,9 @@ __device__ __forceinline__ unsigned long long stamp() {
 //   [32, 36) the defer list's counters (see hpdi_stream_kernel); the list
 //          itself (int32 items, kDeferCap at most) ends the workspace
 constexpr int kWsReady = 8, kWsClaim = 9, kWsStarted = 10, kWsBad = 11;
+// [12] the claim counter as the late launch found it (a diagnostic: the HPDI
+// items the early launch took while the fit ran, tests/test_gpu_paths.py)
+constexpr int kWsEarlyClaimed = 12;
 // the HPDI stream's defer list (hpdi_stream_kernel), on a 128-B line of their
 // own (away from the counters the fit kernel's atomics hit): [32] reservations
 // (+ kDefClosed once the late launch has closed it), [33] slots written, [34]
@@ -1109,6 +1112,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
     }
     // another early wave has deferred already: nothing for this one to do
     if (__hip_atomic_load(ws + kWsEarlyQuit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+  } else if (blockIdx.x == 0 && lane == 0) {
+    __hip_atomic_store(ws + kWsEarlyClaimed, __hip_atomic_load(ws + kWsClaim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   HpdiIO io{};
   io.out = out;
@@ -1636,6 +1642,10 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
     return 0;
   }
   const int64_t n_init = MDFIT_NSUBFIT * n_taxa;
+  // (MDFIT_DEBUG_POISON_LDS: on the caller's stream ahead of K0, so the early
+  // HPDI launch on the side stream starts on the poisoned LDS without the
+  // poison grid delaying it past its wait for the fit kernel's start)
+  mdfit::host::debug_poison(s);
   hipLaunchKernelGGL(mdfit::init_kernel, dim3((unsigned)((n_init + 255) / 256)), dim3(256), 0, s, y, N,
                      n_taxa, out, ws);
   if (int rc = check_launch("init_kernel")) return rc;
@@ -1673,7 +1683,6 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   if (early_per_cu > 0) {
     const int64_t g = std::min<int64_t>(fit_grid(mdfit::hpdi_stream_kernel<true>, n_items, mdfit::kWave, early_per_cu),
                                         kDeferCap / mdfit::kWave);
-    mdfit::host::debug_poison(fork_hp.side());
     hipLaunchKernelGGL(mdfit::hpdi_stream_kernel<true>, dim3((unsigned)g), dim3(mdfit::kWave), 0, fork_hp.side(), N,
                        n_taxa, per, out, pred, ws, (const double*)ready, defer, defer_ticks);
     if (int rc = check_launch("hpdi_stream_kernel")) return rc;

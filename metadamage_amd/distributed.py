@@ -18,11 +18,11 @@ import numpy as np
 
 from . import _lib
 
-# One gathered per-taxon record: the result columns of out (f64[NRES_GATHER]:
-# the 25 fields + 7 reserved) | pred f32[3*30] | status i32.  The 48
-# per-sub-fit diagnostic doubles of out stay on the rank that fitted them, so
-# the collective moves 620 instead of 1004 bytes per taxon.
-NRES_GATHER = _lib.F_DIAG
+# One gathered per-taxon record: the 25 result columns of out
+# (f64[NRES_GATHER]) | pred f32[3*30] | status i32 = 564 bytes.  The record's
+# 7 reserved doubles and its 48 per-sub-fit diagnostic doubles stay on the
+# rank that fitted them (1004 bytes per taxon otherwise).
+NRES_GATHER = _lib.NRESULT
 REC_PRED = _lib.NPRED * _lib.NPOS * 4
 REC_RES = NRES_GATHER * 8
 REC_BYTES = REC_PRED + 4 + REC_RES

@@ -120,13 +120,21 @@ def pack_counts(df: pd.DataFrame, cfg, pinned: bool = False) -> Packed:
     reshaping; anything else is scattered row by row."""
     fwd, rev = cfg.substitution_bases_forward, cfg.substitution_bases_reverse
     tax = df["tax_id"]
+    # rows without a tax_id belong to no taxon: the reference's
+    # groupby("tax_id", observed=True) drops missing keys (fits.py:736-744,
+    # 398-419), so they are dropped here before any index is formed (a -1
+    # index would scatter them onto the last taxon's row)
+    missing = tax.isna().to_numpy()
+    if missing.any():
+        df = df[~missing]
+        tax = df["tax_id"]
     # taxon index in first-appearance order (pd.factorize) and each taxon's first row
     codes = tax.cat.codes.to_numpy() if isinstance(tax.dtype, pd.CategoricalDtype) else None
-    if codes is not None and len(tax.cat.categories) < 2**31 and (codes.size == 0 or codes.min() >= 0):
+    if codes is not None and len(tax.cat.categories) < 2**31:
         from . import ingest
 
         t, first = ingest.first_index(codes, len(tax.cat.categories))
-    else:  # (also a categorical holding a missing tax_id, code -1)
+    else:
         t, _ = pd.factorize(tax.to_numpy())
         t = t.astype(np.int64)
         first = np.flatnonzero(np.r_[True, t[1:] > np.maximum.accumulate(t[:-1])]) if t.size else np.zeros(0, np.int64)
@@ -192,7 +200,6 @@ def fit_packed(p: Packed, opts=None, shard: bool = True):
     import torch
 
     from . import engine
-    from .distributed import alloc_records, gather_records, shard_capacity, shard_range, unpack_gathered
 
     if not torch.cuda.is_available():
         raise _lib.MdfitError("metadamage_amd fits run on MI355X GPUs only (no HIP device visible)")
@@ -211,9 +218,22 @@ def fit_packed(p: Packed, opts=None, shard: bool = True):
     # statistics (ingest.noise) take ~1.5 ms of CPU per 10k taxa on the 16-thread
     # share of a multi-file pipeline that is host-bound
     if not grouped:
-        res = engine.fit_batch_host(p.y, p.N, p.mm, opts, pinned=p.pinned)
-        p.release_pinned()  # (the call synchronised: the device has the counts)
-        return res
+        try:
+            return engine.fit_batch_host(p.y, p.N, p.mm, opts, pinned=p.pinned)
+        finally:
+            p.release_pinned()  # (the call synchronised, or raised: the pinned set goes back either way)
+    try:
+        return _fit_sharded(p, opts, dev, rank, world)
+    finally:
+        p.release_pinned()
+
+
+def _fit_sharded(p: Packed, opts, dev, rank: int, world: int):
+    import torch
+
+    from . import engine
+    from .distributed import alloc_records, gather_records, shard_capacity, shard_range, unpack_gathered
+
     lo, hi = shard_range(p.n_taxa, rank, world)
     if opts is not None:  # the sampler's streams are keyed by the global taxon index
         opts = _lib.MdfitOpts.from_buffer_copy(opts)

@@ -103,10 +103,12 @@ def main(filenames, cfg, opts=None):
                 if packed is not None:
                     packed.release_pinned()
                 continue
-            r = fits.get_fits(df_counts, cfg_f, opts=opts, shard=not shard_files, writer=writer, packed=packed,
-                              deferred=True)
-            if packed is not None:  # (a cache hit never fits it)
-                packed.release_pinned()
+            try:
+                r = fits.get_fits(df_counts, cfg_f, opts=opts, shard=not shard_files, writer=writer, packed=packed,
+                                  deferred=True)
+            finally:
+                if packed is not None:  # (a cache hit never fits it; a failed fit returns it too)
+                    packed.release_pinned()
             # the frames are built (and their saves submitted) on a writer
             # thread while the next file fits
             results[cfg_f.shortname] = pool.submit(r) if callable(r) else r

@@ -61,21 +61,31 @@ def test_packing_matches_group_to_numpyro_data(name, ref_meta, ref_golden):
 
 
 def test_packing_categorical_with_a_missing_tax_id(ref_meta):
-    """A categorical tax_id column holding a missing value (code -1) packs like
-    the same column as plain values (the pd.factorize path), not through the
-    first-appearance index of non-negative codes."""
+    """Rows whose tax_id is missing (a categorical's code -1, or NaN in a plain
+    column) belong to no taxon -- the reference's groupby(observed=True) drops
+    missing keys -- so both forms pack exactly like the table without those
+    rows: no extra taxon, and no other taxon's counts overwritten."""
     name = list(CASES)[0]
     cfg = cfg_for(ref_meta["cases"][name], GOLDEN / CASES[name])
     df = pd.read_parquet(GOLDEN / f"counts_{name}.parquet")
     df["tax_id"] = df["tax_id"].astype(str).astype(object)
-    df.loc[df.index[-30:], "tax_id"] = np.nan  # the last taxon's rows
-    plain = fits.pack_counts(df, cfg)
-    cat = df.copy()
-    cat["tax_id"] = cat["tax_id"].astype("category")
-    assert cat["tax_id"].cat.codes.min() == -1
-    p = fits.pack_counts(cat, cfg)
-    assert p.n_taxa == plain.n_taxa
-    assert (p.y == plain.y).all() and (p.N == plain.N).all()
+    full = fits.pack_counts(df, cfg)
+    assert full.n_taxa >= 2
+    for rows in (slice(-30, None), slice(0, 30)):  # the last taxon's rows, then the first's
+        d = df.copy()
+        d.loc[d.index[rows], "tax_id"] = np.nan
+        ref = fits.pack_counts(d[d["tax_id"].notna()], cfg)
+        kept = list(range(1, full.n_taxa)) if rows.start == 0 else list(range(full.n_taxa - 1))
+        assert ref.n_taxa == full.n_taxa - 1
+        assert (ref.y == full.y[kept]).all() and (ref.N == full.N[kept]).all()
+        cat = d.copy()
+        cat["tax_id"] = cat["tax_id"].astype("category")
+        assert cat["tax_id"].cat.codes.min() == -1
+        for frame in (d, cat):
+            p = fits.pack_counts(frame, cfg)
+            assert p.n_taxa == ref.n_taxa
+            assert (p.y == ref.y).all() and (p.N == ref.N).all() and (p.mm == ref.mm).all()
+            assert [str(x) for x in p.tax_id] == [str(x) for x in ref.tax_id]
 
 
 def test_top_max_fits_matches_reference(ref_meta):

@@ -99,10 +99,69 @@ def test_gloo_shard_and_gather_reproduce_single_process(world, T, async_op):
     np.testing.assert_array_equal(got[2], s)
 
 
+def _c4_worker(rank, world, port, total, share, q):
+    """bench.py's C4 step at world size `world` on gloo: this rank's C4 rows
+    (bench.c4_rows), the fit (the CPU oracle standing in for the kernel),
+    stage, the one gather, unpack on rank 0."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        from metadamage_amd.synthetic import generate
+        from oracle.oracle import OracleLib
+
+        b = generate(share, seed=3)
+        lo, hi, rows = bench.c4_rows(rank, world, total=total, share=share)
+        cap = shard_capacity(total, world)
+        rec = alloc_records(cap, "cpu")
+        rec.buf.zero_()
+        rec.out.zero_()
+        if hi > lo:
+            o, p, s = OracleLib().fit_batch(b.y[rows], b.N[rows], b.mm[rows], threads=1)
+            rec.out[: hi - lo] = torch.from_numpy(o)
+            rec.pred[: hi - lo] = torch.from_numpy(p)
+            rec.status[: hi - lo] = torch.from_numpy(s)
+        parts = gather_records(rec.stage(), cap, rank, world)
+        if rank == 0:
+            q.put(unpack_gathered(parts, total, world))
+        else:
+            assert parts is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,total,share", [(8, 64, 16), (8, 61, 16), (4, 64, 16)])
+def test_bench_c4_step_rehearsal(world, total, share):
+    """The C4 bench step (shard -> stage -> gather -> unpack) at 8 ranks on
+    gloo reproduces the one-process fit of the same global taxa (global taxon
+    i = share row i % share, what c4_one_gpu fits), ragged totals included."""
+    import bench
+    from metadamage_amd.synthetic import generate
+    from oracle.oracle import OracleLib
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c4_worker, args=(r, world, port, total, share, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    _, _, rows = bench.c4_rows(0, 1, total=total, share=share)
+    assert rows.size == total and (rows == np.arange(total) % share).all()
+    b = generate(share, seed=3)
+    o, pr, s = OracleLib().fit_batch(b.y[rows], b.N[rows], b.mm[rows], threads=1)
+    np.testing.assert_array_equal(got[0], o[:, :NRES_GATHER])
+    np.testing.assert_array_equal(got[1], pr)
+    np.testing.assert_array_equal(got[2], s)
+
+
 @pytest.mark.parametrize("n", [5, 6])
 def test_record_views_layout(n):
     rec = alloc_records(n, "cpu")
-    assert rec.buf.numel() == n * REC_BYTES and REC_BYTES == 620
+    assert rec.buf.numel() == n * REC_BYTES and REC_BYTES == 564
     assert rec.out.shape == (n, 80) and rec.res.shape == (n, NRES_GATHER)
     assert rec.pred.shape == (n, 3, 30) and rec.status.shape == (n,)
     assert rec.res.is_contiguous() and rec.pred.is_contiguous() and rec.status.is_contiguous()

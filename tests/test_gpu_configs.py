@@ -73,8 +73,10 @@ def test_c3_nuts_100k(engine, oracle_lib):
     assert (st == 0).all(), np.flatnonzero(st != 0)[:10]  # every taxon OK (as in every box run so far)
     cols = [0, 1, 4, 5, 6, 15, 18, 21]
     bad = np.flatnonzero(~np.isfinite(out[:, cols]).all(1))
-    # (one box run of round 4 saw a non-finite column here, not reproduced in
-    # the runs after it: name the taxa, fields and sub-fit diagnostics if it recurs)
+    # (round 4: a NaN asymmetry here was traced to the post kernel reading an
+    # LDS entry no sub-fit writes; reproduced, fixed in 7a2d388 and guarded by
+    # test_gpu_paths.py::test_poisoned_lds_same_record -- name the taxa, fields
+    # and sub-fit diagnostics if a non-finite column ever shows again)
     assert bad.size == 0, [(int(t), [_lib.RESULT_FIELDS[c] for c in cols if not np.isfinite(out[t, c])],
                             out[t, :25].tolist(), out[t, _lib.F_DIAG:].tolist()) for t in bad[:3]]
     sub = 30_000 + np.arange(64)  # a contiguous subsample (one oracle call, index_base keyed)

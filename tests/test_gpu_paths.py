@@ -281,6 +281,10 @@ def test_poisoned_lds_same_record(torch_dev, monkeypatch, mode, T):
         r = engine.fit_batch_device(ty, tN, tm, opts)
         torch.cuda.synchronize()
         recs.append((r.out.cpu().numpy(), r.pred.cpu().numpy(), r.status.cpu().numpy()))
+        if mode == "map" and T < 60_000:
+            # the poisoned call exercised the streamed early HPDI launch: it had
+            # claimed items by the time the late launch started (workspace int 12)
+            assert int(r.workspace[48:52].view(torch.int32).item()) > 0, poison
     for x, y in zip(*recs):
         assert np.array_equal(x, y, equal_nan=True)
     if mode == "nuts":  # (the columns test_c3_nuts_100k checks)

@@ -147,7 +147,7 @@ def _rank_worker(rank, world, port, files, out_dir, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n_files,world", [(5, 2), (1, 2), (3, 3)])
+@pytest.mark.parametrize("n_files,world", [(5, 2), (1, 2), (3, 3), (10, 8)])
 def test_main_deals_files_to_ranks(tmp_path, n_files, world):
     """At least as many files as ranks: files round-robin, fitted unsharded on
     the owning rank.  Fewer: every rank reads every file and the fit shards
