@@ -490,14 +490,23 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
 #ifdef MDFIT_STAMP
     const unsigned long long e1 = stamp();
 #endif
-    // sums over the slot's positions (all-position fits) or the half's
+    // sums over the slot's positions (all-position fits) or the half's.  PPL 1:
+    // every accumulator's cross-row partner (xor 16, ds_bpermute) is requested
+    // before the first one is used, so the 16 LDS round trips overlap (one
+    // accumulator at a time, each waited for by its own lgkmcnt(0), cost ~1.5k
+    // cycles per trip)
+    if (PPL == 1) {
+      double o[kNAcc];
 #pragma unroll
-    for (int j = 0; j < kNAcc; ++j) {
-      if (PPL == 1) {
-        const double v = opaque(acc[j]);
-        const double o = __shfl_xor(v, 16, 64);
-        acc[j] = gsum<16>(whole ? v + o : v);
-      } else {
+      for (int j = 0; j < kNAcc; ++j) acc[j] = opaque(acc[j]);
+#pragma unroll
+      for (int j = 0; j < kNAcc; ++j) o[j] = __shfl_xor(acc[j], 16, 64);
+#pragma unroll
+      for (int j = 0; j < kNAcc; ++j) acc[j] = gsum<16>(whole ? acc[j] + o[j] : acc[j]);
+    }
+    if (PPL == 2) {
+#pragma unroll
+      for (int j = 0; j < kNAcc; ++j) {
         const double s8 = gsum<8>(acc[j]);
         const double s16 = s8 + dpp<0x140>(s8);  // row_mirror: the other half's sum
         acc[j] = whole ? s16 : s8;
@@ -522,6 +531,12 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       const bool pprobe = esc & kEscPolishProbe;
       // the gradient fallback's re-evaluation at u: its g gives the direction
       const bool gprobe = esc & kEscGradProbe;
+      // the trial just evaluated was a full Newton step (not a probe, the first
+      // point, a backtracked / escape / gradient-fallback / flat-tail-rescue
+      // step), and its size: the quadratic-contraction stop below
+      const bool newton_trial = !(probed || pprobe || gprobe) && !first &&
+                                !(esc & (kEscNc | kEscGrad | kEscRelax)) && t == 1.0;
+      const double dprev = t * maxabs4(d);
       esc &= ~(kEscProbe | kEscPolishProbe | kEscGradProbe);
       if (probed || pprobe || gprobe) {
         accept = true;
@@ -575,7 +590,16 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
             }
           } else {
             esc = ind ? esc | kEscIndef : esc & ~kEscIndef;
-            if (maxabs4(d) <= tol) {
+            const double dn = maxabs4(d);
+            if (dn <= tol) {
+              done = true;
+              status = MDFIT_OK;
+            } else if (newton_trial && !ind && kQuadK * dn * dn <= tol && dn <= kQuadK * dprev * dprev) {
+              // MDFIT-MAP v1.1 (oracle: fit_one): converged by quadratic
+              // contraction -- the step is taken without evaluating its end
+              // point (the error left is O(|d|^2) <= tol)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) u[j] = clampd(u[j] + d[j], kULo[j], kUHi[j]);
               done = true;
               status = MDFIT_OK;
             }

@@ -28,6 +28,7 @@ constexpr double kUHi[4] = {25.0, 25.0, 0.999, 20.0};
 constexpr double kEpsAct = 1e-8;
 constexpr double kNoiseF = 1.4e-14;  // objective rounding scale (oracle: NOISE_F)
 constexpr double kPgTol = 1e-6;      // exhausted line search + |proj. grad| below: converged (oracle: PG_TOL)
+constexpr double kQuadK = 10.0;      // the quadratic-contraction stop of fit_kernel (oracle: QUAD_K)
 
 // ---------------------------------------------------------------------------
 // cross-lane sums inside aligned groups of G lanes (G = 2 ... 64)
