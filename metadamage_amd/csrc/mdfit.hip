@@ -286,6 +286,18 @@ __device__ __forceinline__ void hpdi_position(const HpdiIO& io, int64_t item, bo
   }
 }
 
+#ifndef MDFIT_LDS_SUMS
+#define MDFIT_LDS_SUMS 1  // fit_kernel's sums through LDS (0: the register butterfly; bitwise-identical)
+#endif
+
+// the butterfly's summation tree over 8 / 16 values in lane order: pairs
+// (xor 1), pairs of pairs (xor 2), the two quads (half mirror), the two halves
+// (mirror) -- sets, so the order inside each add does not matter
+__device__ __forceinline__ double tree8(const double* x) {
+  return ((x[0] + x[1]) + (x[2] + x[3])) + ((x[4] + x[5]) + (x[6] + x[7]));
+}
+__device__ __forceinline__ double tree16(const double* x) { return tree8(x) + tree8(x + 8); }
+
 template <int PPL>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_FIT_WAVES_PER_EU)))
 void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN, int64_t T,
@@ -340,6 +352,13 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
   pb.k = kB_all;
   pa.pmd = pb.pmd = true;
 
+#if MDFIT_LDS_SUMS
+  // the sums' LDS: the lanes' terms accumulator-major (row stride padded by 2
+  // doubles: a row's 16 lanes then read 16 consecutive 16-B slots, no bank
+  // conflict) and the finished sums (PPL 2: one set per half)
+  __shared__ __attribute__((aligned(16))) double sAcc[kNAcc][kWave + 2];
+  __shared__ __attribute__((aligned(16))) double sSum[2][kWave];
+#endif
   // the HPDI stream kernel running beside this one waits only once it has
   // seen this flag (no wait on a kernel that may not be running)
   if (blockIdx.x == 0 && lane == 0)
@@ -408,7 +427,9 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
     }
 #ifdef MDFIT_STAMP
     const unsigned long long a1 = stamp();
+#ifndef MDFIT_STAMP2
     st_claim1 += a1 - a0;
+#endif
 #endif
     // ---- 2. a finished all-position fit continues with its fwd/rev pair ----
     const bool next = mode == kNextPair;
@@ -440,7 +461,7 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         }  // else: warm start at the all-position mode, u
       }
     }
-#ifdef MDFIT_STAMP
+#if defined(MDFIT_STAMP) && !defined(MDFIT_STAMP2)
     st_claim2 += stamp() - a1;
 #endif
     if (starting) {
@@ -490,11 +511,55 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
 #ifdef MDFIT_STAMP
     const unsigned long long e1 = stamp();
 #endif
-    // sums over the slot's positions (all-position fits) or the half's.  PPL 1:
-    // every accumulator's cross-row partner (xor 16, ds_bpermute) is requested
-    // before the first one is used, so the 16 LDS round trips overlap (one
-    // accumulator at a time, each waited for by its own lgkmcnt(0), cost ~1.5k
-    // cycles per trip)
+    // sums over the slot's positions (all-position fits) or the half's
+#if MDFIT_LDS_SUMS
+    // Through LDS, accumulator-major: every lane writes its 16 terms to
+    // sAcc[j][lane], then lane i of a row forms the row's sum of accumulator i
+    // (tree16 / tree8: the butterfly's summation tree, so the same bits as the
+    // register butterfly below and in both layouts), and the sums come back to
+    // every lane of the row from sSum.  ~60 VALU per trip instead of ~240 DPP
+    // moves and adds.
+#pragma unroll
+    for (int j = 0; j < kNAcc; ++j) sAcc[j][lane] = acc[j];
+    __syncthreads();
+    if (PPL == 1) {
+      // own row (the sub-fit of a pair half; for an all-position fit both rows
+      // form the same sum: x_k = row 0 + row 1 at position k, as the butterfly's
+      // first step)
+      const double* a = &sAcc[jh][leader + 16 * h];
+      const double* b = &sAcc[jh][leader + 16 * (1 - h)];
+      double x[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const double ak = a[k], bk = b[k];
+        x[k] = whole ? ak + bk : ak;
+      }
+      sSum[0][lane] = tree16(x);
+      __syncthreads();
+      const double* src = &sSum[0][leader + 16 * h];
+#pragma unroll
+      for (int j = 0; j < kNAcc; ++j) acc[j] = src[j];
+    } else {
+      // lane r of a 16-lane slot: accumulator r over each 8-lane half (the pair
+      // sub-fits' sums), and their sum (the all-position fit's)
+      const double* a = &sAcc[r][leader];
+      double x[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) x[k] = a[k];
+      const double A0 = tree8(x), A1 = tree8(x + 8);
+      const double S = A0 + A1;
+      sSum[0][lane] = whole ? S : A0;
+      sSum[1][lane] = whole ? S : A1;
+      __syncthreads();
+      const double* src = &sSum[whole ? 0 : h][leader];
+#pragma unroll
+      for (int j = 0; j < kNAcc; ++j) acc[j] = src[j];
+    }
+#else
+    // PPL 1: every accumulator's cross-row partner (xor 16, ds_bpermute) is
+    // requested before the first one is used, so the 16 LDS round trips
+    // overlap (one accumulator at a time, each waited for by its own
+    // lgkmcnt(0), cost ~1.5k cycles per trip)
     if (PPL == 1) {
       double o[kNAcc];
 #pragma unroll
@@ -512,6 +577,7 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         acc[j] = whole ? s16 : s8;
       }
     }
+#endif
 #ifdef MDFIT_STAMP
     const unsigned long long e2 = stamp();
 #endif
@@ -522,6 +588,11 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       finish_eval(pa.pmd, th, acc, tr);
       ++evals;
       const double pgt = pgnorm(ut, tr.g);  // projected gradient at the trial point
+#ifdef MDFIT_STAMP2
+      // (-DMDFIT_STAMP2: slots 6 / 7 of the stamp record split the Newton
+      // logic -- finish_eval + pgnorm, and newton_dir)
+      st_claim1 += stamp() - e2;
+#endif
       bool accept = false, done = false;
       // the saddle escape's re-evaluation at u (same F, g, H as the current
       // point) goes through the acceptance below; its H gives the direction
@@ -563,7 +634,13 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         if (!done) {
           // (the gradient fallback's probe: the projected-gradient direction
           // replaces the Newton step; oracle: fit_one)
-          const bool ind = newton_dir(pa.pmd, u, tr.g, tr.H, pgt, d, probed);
+#ifdef MDFIT_STAMP2
+          const unsigned long long nd0 = stamp();
+#endif
+          const bool ind = newton_dir<kHalf>(pa.pmd, u, tr.g, tr.H, pgt, d, probed);
+#ifdef MDFIT_STAMP2
+          st_claim2 += stamp() - nd0;
+#endif
           const bool gok = gprobe && pg_direction(u, tr.g, d);
           curG3 = tr.g[3];
           curGd = tr.g[0] * d[0] + tr.g[1] * d[1] + tr.g[2] * d[2] + tr.g[3] * d[3];

@@ -376,7 +376,7 @@ __device__ __forceinline__ int chol4(const bool fr[4], const double H[10], doubl
       if (!fr[j] || !fr[m]) s = (j == m) ? 1.0 : 0.0;
       else s = H[hidx(m, j)] + ((j == m) ? mu : 0.0);
 #pragma unroll
-      for (int p = 0; p < m; ++p) s -= L[hidx(p, j)] * L[hidx(p, m)];
+      for (int p = 0; p < m; ++p) s = fma(-L[hidx(p, j)], L[hidx(p, m)], s);  // explicit: the same rounding in every instance
       if (j == m) {
         if (!(s > 0.0) && jf < 0) jf = j;
         const double sp = fmax(s, 1e-300);
@@ -421,6 +421,15 @@ __device__ __forceinline__ void free_set(bool pmd, const double u[4], const doub
 // saddle escape; oracle: nc_direction): the unshifted Cholesky's first
 // non-positive pivot s_j with the rows above it gives z = (-L^-T l, 1, 0..),
 // z'Hz = s_j <= 0, scaled to max-norm 1 and signed downhill.
+//
+// G: the lanes that hold this fit's (replicated) state -- an aligned group.
+// An indefinite H is shifted by mu_a = 1e-10 scale x 10^(a-1) for the first a
+// = 1, 2, ... whose Cholesky succeeds (oracle: direction(), the same mu by the
+// same repeated products); the group's lanes try attempts 1..G at once, lane k
+// attempt k+1 (one Cholesky's latency instead of up to G in a row), and take
+// the step from the lane of the first success; past G the rest of the
+// sequence runs replicated, as before (rare: ~1 % of shifted systems at G = 8).
+template <int G>
 __device__ __forceinline__ bool newton_dir(bool pmd, const double u[4], const double g[4],
                                            const double H[10], double w, double d[4], bool want_nc = false) {
   bool fr[4];
@@ -450,14 +459,43 @@ __device__ __forceinline__ bool newton_dir(bool pmd, const double u[4], const do
     return true;
   }
   bool ok = !indef;
-  if (!ok) {  // indefinite: shift the diagonal by 1e-10 * scale, x10 per retry
+  // the solve with the accepted factor: every lane of a group that needed a
+  // shift solves with its own attempt's factor, then takes the winner's step
+  int src = -1;  // >= 0: the lane (absolute) whose step this lane takes
+  if (__any(!ok)) {
     double sc = 0.0;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       if (fr[j]) sc = fmax(sc, fabs(H[hidx(j, j)]));
     if (sc == 0.0) sc = 1.0;
+    const int kl = (int)(threadIdx.x & (G - 1));
+    const int gbase = (int)(threadIdx.x & ~(G - 1));
     double mu = 1e-10 * sc;
-    for (int attempt = 1; attempt < 40 && !ok; ++attempt, mu *= 10.0) ok = chol4(fr, H, mu, L, iL) < 0;
+#pragma unroll
+    for (int i = 1; i < G; ++i) mu = i <= kl ? mu * 10.0 : mu;  // attempt kl + 1
+    double L2[10], iL2[4];
+    // (mu opaque: a product the compiler may not fuse into the Cholesky's
+    // diagonal add -- it would round differently in the parallel and the
+    // sequential instance, and the two layouts reach them at different attempts)
+    const bool ok2 = !ok && chol4(fr, H, opaque(mu), L2, iL2) < 0;
+    const unsigned long long gm = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << gbase;
+    const unsigned long long okm = __ballot(ok2) & gm;
+    if (!ok) {
+      if (okm != 0ull) {
+        ok = true;
+        src = __ffsll(okm) - 1;
+#pragma unroll
+        for (int j = 0; j < 10; ++j) L[j] = L2[j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) iL[j] = iL2[j];
+      } else {  // attempts G+1 .. 39, replicated on the group's lanes
+        mu = 1e-10 * sc;
+#pragma unroll 1
+        for (int i = 1; i < G; ++i) mu *= 10.0;  // attempt G
+        mu *= 10.0;
+        for (int attempt = G + 1; attempt < 40 && !ok; ++attempt, mu *= 10.0) ok = chol4(fr, H, opaque(mu), L, iL) < 0;
+      }
+    }
   }
   if (!ok) {
 #pragma unroll
@@ -468,16 +506,21 @@ __device__ __forceinline__ bool newton_dir(bool pmd, const double u[4], const do
     for (int j = 0; j < 4; ++j) {  // L z = -g (free rows)
       double s = fr[j] ? -g[j] : 0.0;
 #pragma unroll
-      for (int p = 0; p < j; ++p) s -= L[hidx(p, j)] * z[p];
+      for (int p = 0; p < j; ++p) s = fma(-L[hidx(p, j)], z[p], s);
       z[j] = s * iL[j];
     }
 #pragma unroll
     for (int j = 3; j >= 0; --j) {  // L^T d = z
       double s = z[j];
 #pragma unroll
-      for (int p = j + 1; p < 4; ++p) s -= L[hidx(j, p)] * d[p];
+      for (int p = j + 1; p < 4; ++p) s = fma(-L[hidx(j, p)], d[p], s);
       d[j] = s * iL[j];
     }
+  }
+  if (__any(src >= 0)) {
+    const int from = src >= 0 ? src : (int)threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) d[j] = __shfl(d[j], from, 64);
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j)

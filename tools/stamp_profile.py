@@ -62,7 +62,7 @@ def main() -> None:
         for j, lab in ((3, "fetch"), (0, "eval"), (1, "reduce"), (2, "logic")):
             print(f"   {lab:7s} {w[:, j].mean() / w[:, 4].mean():9.0f} cyc/trip  "
                   f"{100 * w[:, j].sum() / tot.sum():5.1f}%")
-        print(f"   claims: all-position {w[:, 6].sum() / tot.sum() * 100:5.1f}%  ring {w[:, 7].sum() / tot.sum() * 100:5.1f}%  "
+        print(f"   claims or (STAMP2) finish_eval+pgnorm {w[:, 6].sum() / tot.sum() * 100:5.1f}%  newton_dir {w[:, 7].sum() / tot.sum() * 100:5.1f}%  "
               f"(of the wave time; includes idle-trip polling)")
     evals = out[:, 32 + 5::8][:, :6]
     print("evals per sub-fit mean:", np.round(evals.mean(0), 2), " max:", evals.max(0))
