@@ -489,22 +489,43 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
 #pragma unroll
     for (int j = 0; j < kNAcc; ++j) acc[j] = 0.0;
     const int accf = (esc & kEscPolish) != 0u;
+    // every slot of the wave fits model_null: a, b from the pads (point_accum)
+    const bool null_wave = !__any(pa.pmd != 0);
     if (PPL == 1) {
-      point_accum<true>(pa, th, acc, accf);
+      point_accum<true>(pa, th, acc, accf, null_wave);
     } else {
       // lg3(phi) from a pad: lane 15's point b (all-position: both halves;
-      // pair: the reverse half), lane 7's point b (pair: the forward half)
-      const LG3 t3b = lg3<true, MDFIT_TLOG_FIT>(pb.N + th.phi);
+      // pair: the reverse half), lane 7's point b (pair: the forward half);
+      // for model_null also lg3(a), lg3(b) (point_accum: null_row)
       const bool src15 = whole || h == 1;
-      LG3 t6;
-      t6.l = src15 ? rowb<15>(t3b.l) : rowb<7>(t3b.l);
-      t6.p = src15 ? rowb<15>(t3b.p) : rowb<7>(t3b.p);
-      t6.q = src15 ? rowb<15>(t3b.q) : rowb<7>(t3b.q);
-      point_contrib(pa, th, lg3<true, MDFIT_TLOG_FIT>(pa.N + th.phi), t6, acc, accf);
+      auto pad3 = [&](const LG3& v) -> LG3 { return src15 ? rowb3<15>(v) : rowb3<7>(v); };
+      const PointArgs gb = point_args(pb, th);
+      const LG3 t3b = lg3<true, MDFIT_TLOG_FIT>(pb.N + th.phi);
+      const LG3 t6 = pad3(t3b);
+      const LG3 tb1 = lg3<true, MDFIT_TLOG_FIT>(pb.y + gb.a);
+      const LG3 tb2 = lg3<true, MDFIT_TLOG_FIT>(pb.N - pb.y + gb.b);
+      LG3 tb4, tb5;
+      if (null_wave) {
+        tb4 = pad3(tb1);
+        tb5 = pad3(tb2);
+      } else {
+        tb4 = lg3<true, MDFIT_TLOG_FIT>(gb.a);
+        tb5 = lg3<true, MDFIT_TLOG_FIT>(gb.b);
+      }
       double accb[kNAcc];
 #pragma unroll
       for (int j = 0; j < kNAcc; ++j) accb[j] = 0.0;
-      point_contrib(pb, th, t3b, t6, accb, accf);
+      point_finish(pb, th, gb, tb1, tb2, t3b, tb4, tb5, t6, accb, accf);
+      const PointArgs ga = point_args(pa, th);
+      const LG3 ta3 = lg3<true, MDFIT_TLOG_FIT>(pa.N + th.phi);
+      const LG3 ta1 = lg3<true, MDFIT_TLOG_FIT>(pa.y + ga.a);
+      const LG3 ta2 = lg3<true, MDFIT_TLOG_FIT>(pa.N - pa.y + ga.b);
+      LG3 ta4 = tb4, ta5 = tb5;  // (null: a, b are the half's; PMD: the point's own)
+      if (!null_wave) {
+        ta4 = lg3<true, MDFIT_TLOG_FIT>(ga.a);
+        ta5 = lg3<true, MDFIT_TLOG_FIT>(ga.b);
+      }
+      point_finish(pa, th, ga, ta1, ta2, ta3, ta4, ta5, t6, acc, accf);
 #pragma unroll
       for (int j = 0; j < kNAcc; ++j) acc[j] = opaque(acc[j]) + opaque(accb[j]);
     }
@@ -1816,15 +1837,24 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   // one left); they write disjoint fields of the record and join before the
   // call returns
   ForkScope fork_as(fk, s, 1);
-  mdfit::host::debug_poison(fork_as.side());
-  hipLaunchKernelGGL(mdfit::assemble_kernel, dim3((unsigned)n_taxa), dim3(mdfit::kWave), 0, fork_as.side(), y, N,
+  // Below kStreamMaxTaxa the record assembly follows the fit on the caller's
+  // stream (it starts as soon as the fit ends; on the side stream it waited
+  // ~30 us longer for the fork event) and the HPDI's late launch -- a short
+  // drain of what the early launch left -- takes the side stream;
+  // MDFIT_ASM_SIDE=1 restores the old placement (A/B).  From kStreamMaxTaxa
+  // the HPDI (K4a -> K4b) is the long part and keeps the caller's stream.
+  const bool asm_main = stream && env_int("MDFIT_ASM_SIDE", 0) == 0;
+  const hipStream_t s_asm = asm_main ? s : fork_as.side();
+  const hipStream_t s_hp = asm_main ? fork_as.side() : s;
+  mdfit::host::debug_poison(s_asm);
+  hipLaunchKernelGGL(mdfit::assemble_kernel, dim3((unsigned)n_taxa), dim3(mdfit::kWave), 0, s_asm, y, N,
                      mm, n_taxa, out, pred, status);
   if (int rc = check_launch("assemble_kernel")) return rc;
   if (stream) {
     const int64_t g = fit_grid(mdfit::hpdi_stream_kernel<false>, n_items, mdfit::kWave,
                                env_int("MDFIT_HPDI_WAVES_PER_CU", 0));
-    mdfit::host::debug_poison(s);
-    hipLaunchKernelGGL(mdfit::hpdi_stream_kernel<false>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s, N, n_taxa, per,
+    mdfit::host::debug_poison(s_hp);
+    hipLaunchKernelGGL(mdfit::hpdi_stream_kernel<false>, dim3((unsigned)g), dim3(mdfit::kWave), 0, s_hp, N, n_taxa, per,
                        out, pred, ws, (const double*)ready, defer, defer_ticks);
     if (int rc = check_launch("hpdi_stream_kernel")) return rc;
   } else {

@@ -176,9 +176,38 @@ struct PointData {
   int pmd;    // lane group fits model_PMD (else model_null)
 };
 
+// A point's D(z) and its derivatives at theta, and the beta-binomial
+// parameters a = D phi, b = (1 - D) phi.
+struct PointArgs {
+  double D, Dq, DA, Dc, Dqq, DqA, omD, a, b;
+};
+__device__ __forceinline__ PointArgs point_args(const PointData& pd, const Theta& th) {
+#pragma clang fp contract(off)  // (every fusion explicit: the same bits in both lane layouts)
+  PointArgs r;
+  if (pd.pmd) {
+    const double kk = (double)pd.k;
+    const double w = powk(th.omq, pd.k);  // (1-q)^k
+    const double wq = w * th.iomq;        // (1-q)^(k-1)
+    r.D = fma(th.A, w, th.c);
+    r.DA = w;
+    r.Dc = 1.0;
+    r.Dq = pd.k >= 1 ? -th.A * kk * wq : 0.0;
+    r.DqA = pd.k >= 1 ? -kk * wq : 0.0;
+    r.Dqq = pd.k >= 2 ? th.A * kk * (kk - 1.0) * (wq * th.iomq) : 0.0;
+  } else {
+    r.D = th.q;
+    r.Dq = 1.0;
+    r.DA = r.Dc = r.Dqq = r.DqA = 0.0;
+  }
+  r.omD = 1.0 - r.D;
+  r.a = r.D * th.phi;
+  r.b = r.omD * th.phi;
+  return r;
+}
+
 // One point's contribution at theta, ADDED to acc (same formulas as
-// oracle/mdfit_oracle.c evaluate(); derivation in DESIGN.md §3), given the
-// point's t3 = (lnGamma, psi, psi1)(N + phi) and t6 = the same at phi.
+// oracle/mdfit_oracle.c evaluate(); derivation in DESIGN.md §3), from the
+// (lnGamma, psi, psi1) triples t1..t6 at y+a, N-y+b, N+phi, a, b, phi.
 // Returns the point's log-likelihood (without log C(N,y)).
 //
 // accf (the polish phase of the fit, oracle: evaluate(accf = 1)): the value
@@ -187,35 +216,14 @@ struct PointData {
 // acc[1] the sum of its three |R| terms: F then resolves ~1e-10 instead of the
 // ~1e-6 of a sum of ~N ln N-sized lnGamma values.  Gradient and Hessian terms
 // are the same in both forms.
-__device__ __forceinline__ double point_contrib(const PointData& pd, const Theta& th, const LG3& t3,
-                                               const LG3& t6, double acc[kNAcc], int accf = 0) {
-  double D, Dq, DA, Dc, Dqq, DqA;
-  if (pd.pmd) {
-    const double kk = (double)pd.k;
-    const double w = powk(th.omq, pd.k);  // (1-q)^k
-    const double wq = w * th.iomq;        // (1-q)^(k-1)
-    D = fma(th.A, w, th.c);
-    DA = w;
-    Dc = 1.0;
-    Dq = pd.k >= 1 ? -th.A * kk * wq : 0.0;
-    DqA = pd.k >= 1 ? -kk * wq : 0.0;
-    Dqq = pd.k >= 2 ? th.A * kk * (kk - 1.0) * (wq * th.iomq) : 0.0;
-  } else {
-    D = th.q;
-    Dq = 1.0;
-    DA = Dc = Dqq = DqA = 0.0;
-  }
+__device__ __forceinline__ double point_finish(const PointData& pd, const Theta& th, const PointArgs& pa,
+                                              const LG3& t1, const LG3& t2, const LG3& t3, const LG3& t4,
+                                              const LG3& t5, const LG3& t6, double acc[kNAcc], int accf = 0) {
+#pragma clang fp contract(off)  // (every fusion explicit: the same bits in both lane layouts)
+  const double D = pa.D, omD = pa.omD, a = pa.a, b = pa.b;
   const double phi = th.phi;
-  const double omD = 1.0 - D;
-  const double a = D * phi, b = omD * phi;
-  // paired so that each pair's lnGamma / psi / psi1 difference is formed as
-  // soon as both halves exist (fewer live registers)
-  const LG3 t1 = lg3<true, MDFIT_TLOG_FIT>(pd.y + a);
-  const LG3 t4 = lg3<true, MDFIT_TLOG_FIT>(a);
   const double la = t1.l - t4.l, Pa = t1.p - t4.p, Qa = t1.q - t4.q;
   double mag = fabs(t1.l) + fabs(t4.l);
-  const LG3 t2 = lg3<true, MDFIT_TLOG_FIT>(pd.N - pd.y + b);
-  const LG3 t5 = lg3<true, MDFIT_TLOG_FIT>(b);
   const double lb = t2.l - t5.l, Pb = t2.p - t5.p, Qb = t2.q - t5.q;
   mag += fabs(t2.l) + fabs(t5.l);
   const double lS = t3.l - t6.l, S = t6.p - t3.p, S1 = t6.q - t3.q;
@@ -226,51 +234,67 @@ __device__ __forceinline__ double point_contrib(const PointData& pd, const Theta
     ell = (r1 + r2) - r3;
     mag = (fabs(r1) + fabs(r2)) + fabs(r3);
   }
+  const double Dq = pa.Dq, DA = pa.DA, Dc = pa.Dc, Dqq = pa.Dqq, DqA = pa.DqA;
   const double lD = phi * (Pa - Pb);
-  const double lF = D * Pa + omD * Pb + S;
-  const double lDD = phi * phi * (Qa + Qb);
-  const double lDF = (Pa - Pb) + phi * (D * Qa - omD * Qb);
-  const double lFF = D * D * Qa + omD * omD * Qb + S1;
+  const double lF = fma(D, Pa, fma(omD, Pb, S));
+  const double lDD = (phi * phi) * (Qa + Qb);
+  const double lDF = fma(phi, fma(D, Qa, -(omD * Qb)), Pa - Pb);
+  const double lFF = fma(D * D, Qa, fma(omD * omD, Qb, S1));
   if (pd.valid) {
+    const double lDDq = lDD * Dq, lDDA = lDD * DA;
     acc[0] += ell;
     acc[1] += mag;
-    acc[2] += lD * Dq;
-    acc[3] += lD * DA;
-    acc[4] += lD * Dc;
+    acc[2] = fma(lD, Dq, acc[2]);
+    acc[3] = fma(lD, DA, acc[3]);
+    acc[4] = fma(lD, Dc, acc[4]);
     acc[5] += lF;
-    acc[6] += lDD * Dq * Dq + lD * Dqq;
-    acc[7] += lDD * Dq * DA + lD * DqA;
-    acc[8] += lDD * Dq * Dc;
-    acc[9] += lDF * Dq;
-    acc[10] += lDD * DA * DA;
-    acc[11] += lDD * DA * Dc;
-    acc[12] += lDF * DA;
-    acc[13] += lDD * Dc * Dc;
-    acc[14] += lDF * Dc;
+    acc[6] = fma(lDDq, Dq, fma(lD, Dqq, acc[6]));
+    acc[7] = fma(lDDq, DA, fma(lD, DqA, acc[7]));
+    acc[8] = fma(lDDq, Dc, acc[8]);
+    acc[9] = fma(lDF, Dq, acc[9]);
+    acc[10] = fma(lDDA, DA, acc[10]);
+    acc[11] = fma(lDDA, Dc, acc[11]);
+    acc[12] = fma(lDF, DA, acc[12]);
+    acc[13] = fma(lDD * Dc, Dc, acc[13]);
+    acc[14] = fma(lDF, Dc, acc[14]);
     acc[15] += lFF;
   }
   return ell;
 }
 
-// One point's contribution (point_contrib), t3 and t6 computed here.
+// a triple broadcast from lane N of every 16-lane DPP row
+template <int N>
+__device__ __forceinline__ LG3 rowb3(const LG3& t) {
+  return {rowb<N>(t.l), rowb<N>(t.p), rowb<N>(t.q)};
+}
+
+// One point's contribution (point_finish): its lnGamma triples computed here.
 //
 // kRowPhi: the (lnGamma, psi, psi1) triple at phi is taken from lane 15 of
 // the 16-lane row -- a pad lane (N = 0) whose lg3(N + phi) IS lg3(phi),
 // bitwise -- so a point costs 5 lg3 instead of 6 (row-collective then: all
 // lanes active, lane 15 of every row a pad holding the row's phi).
+// null_row (wave-uniform; kRowPhi only): every row fits model_null, where a =
+// q phi and b = (1-q) phi are the same at every point of the row, and the pad
+// lane's lg3(y + a), lg3(N - y + b) ARE lg3(a), lg3(b), bitwise: broadcast
+// from it, 3 lg3 per point instead of 5.
 template <bool kRowPhi = false>
 __device__ __forceinline__ double point_accum(const PointData& pd, const Theta& th,
-                                              double acc[kNAcc], int accf = 0) {
+                                              double acc[kNAcc], int accf = 0, bool null_row = false) {
+  const PointArgs pa = point_args(pd, th);
   const LG3 t3 = lg3<true, MDFIT_TLOG_FIT>(pd.N + th.phi);
-  LG3 t6;
-  if (kRowPhi) {
-    t6.l = rowb<15>(t3.l);
-    t6.p = rowb<15>(t3.p);
-    t6.q = rowb<15>(t3.q);
+  const LG3 t6 = kRowPhi ? rowb3<15>(t3) : lg3<true, MDFIT_TLOG_FIT>(th.phi);
+  const LG3 t1 = lg3<true, MDFIT_TLOG_FIT>(pd.y + pa.a);
+  const LG3 t2 = lg3<true, MDFIT_TLOG_FIT>(pd.N - pd.y + pa.b);
+  LG3 t4, t5;
+  if (kRowPhi && null_row) {
+    t4 = rowb3<15>(t1);
+    t5 = rowb3<15>(t2);
   } else {
-    t6 = lg3<true, MDFIT_TLOG_FIT>(th.phi);
+    t4 = lg3<true, MDFIT_TLOG_FIT>(pa.a);
+    t5 = lg3<true, MDFIT_TLOG_FIT>(pa.b);
   }
-  return point_contrib(pd, th, t3, t6, acc, accf);
+  return point_finish(pd, th, pa, t1, t2, t3, t4, t5, t6, acc, accf);
 }
 
 // Pointwise log-likelihood of one point at a mode for the record assembly

@@ -1147,6 +1147,7 @@ __device__ __forceinline__ PotC potential_cd(const PointData pt[PPL], double x, 
   const double delta = bc(e, I3{}), v3 = bc(x, I3{});
   const double phi = delta + 2.0;
   const bool pmd = pt[0].pmd;
+  const bool null_wave = !__any(pmd);  // (PPL 1: the pad lanes then give lg3(a), lg3(b))
   const double A = pmd ? A0 : 0.0, cc = pmd ? c0 : 0.0;
   double lprior = prq + v3 - delta * 1e-3;
   if (pmd) lprior += prA + prc;
@@ -1182,10 +1183,24 @@ __device__ __forceinline__ PotC potential_cd(const PointData pt[PPL], double x, 
     bad_lane = bad_lane || (pd.valid && !(D < 1.0));
     const double a = D * phi, b = (1.0 - D) * phi;
     const LG3 t1 = lg3<false, MDFIT_TLOG_NUTS>(pd.y + a);
-    const LG3 t4 = lg3<false, MDFIT_TLOG_NUTS>(a);
+    LG3 t4;
+    if (PPL == 1 && null_wave) {
+      // every chain of the wave samples model_null: a = q phi is the row's, and
+      // the pad lane's lg3(0 + a) IS lg3(a), bitwise (likewise b below)
+      t4.l = rowb<15>(t1.l);
+      t4.p = rowb<15>(t1.p);
+    } else {
+      t4 = lg3<false, MDFIT_TLOG_NUTS>(a);
+    }
     const double la = t1.l - t4.l, Pa = t1.p - t4.p;
     const LG3 t2 = lg3<false, MDFIT_TLOG_NUTS>(pd.N - pd.y + b);
-    const LG3 t5 = lg3<false, MDFIT_TLOG_NUTS>(b);
+    LG3 t5;
+    if (PPL == 1 && null_wave) {
+      t5.l = rowb<15>(t2.l);
+      t5.p = rowb<15>(t2.p);
+    } else {
+      t5 = lg3<false, MDFIT_TLOG_NUTS>(b);
+    }
     const double lb = t2.l - t5.l, Pb = t2.p - t5.p;
     const LG3 t3 = (PPL == 1 || pi == 1) ? t3b : lg3<false, MDFIT_TLOG_NUTS>(pd.N + phi);
     const double ell = (la + lb) - (t3.l - t6l);

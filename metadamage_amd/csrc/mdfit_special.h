@@ -47,6 +47,7 @@ __device__ __forceinline__ double rcp1(double x) {
 // R a degree-7 minimax polynomial in s^2 -- Cody & Waite / the fdlibm scheme).
 // 0 -> -inf, +inf -> +inf, negative / NaN -> NaN.
 __device__ __forceinline__ double flog(double x) {
+#pragma clang fp contract(off)  // (every fusion explicit: the same bits in every inlined instance)
   constexpr double kLn2Hi = 6.93147180369123816490e-01;  // high 32 bits of ln 2
   constexpr double kLn2Lo = 1.90821492927058770002e-10;  // ln 2 - kLn2Hi
   constexpr double kSqrtHalf = 0.70710678118654752440;
@@ -58,16 +59,15 @@ __device__ __forceinline__ double flog(double x) {
   const double f = m - 1.0;  // exact
   const double s = f * rcp(2.0 + f);
   const double z = s * s, w = z * z;
-  const double t1 = w * fma(w, fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01),
-                            3.999999999940941908e-01);
   const double t2 =
       z * fma(w, fma(w, fma(w, 1.479819860511658591e-01, 1.818357216161805012e-01),
                      2.857142874366239149e-01),
               6.666666666666735130e-01);
-  const double R = t2 + t1;
+  const double R = fma(w, fma(w, fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01),
+                              3.999999999940941908e-01), t2);
   const double hfsq = 0.5 * f * f;
   const double de = (double)e;
-  const double r = de * kLn2Hi - ((hfsq - fma(s, hfsq + R, de * kLn2Lo)) - f);
+  const double r = fma(de, kLn2Hi, -((hfsq - fma(s, hfsq + R, de * kLn2Lo)) - f));
   const bool normal = x > 0.0 && x < INFINITY;
   return normal ? r : (x == 0.0 ? -INFINITY : (x == INFINITY ? x : NAN));
 }
@@ -95,6 +95,7 @@ namespace mdfit {
 // (pre-scaled) -- lnGamma's shift product, which is 0 at a = 0.
 template <bool kZero = false>
 __device__ __forceinline__ double flog_t(double x) {
+#pragma clang fp contract(off)
   constexpr double kLn2Hi = 6.93147180369123816490e-01;
   constexpr double kLn2Lo = 1.90821492927058770002e-10;
   double xn = x;
@@ -119,12 +120,13 @@ __device__ __forceinline__ double flog_t(double x) {
   const double de = (double)e;
   // e ln2_hi is exact (ln2_hi has 21 trailing zero bits): one rounding at the
   // end, as fdlibm's, instead of two (~0.5 ulp typical instead of ~1)
-  const double y = de * kLn2Hi + (t.y + (r + fma(r2, q, de * kLn2Lo)));
+  const double y = fma(de, kLn2Hi, t.y + (r + fma(r2, q, de * kLn2Lo)));
   return kZero ? (x > 0.0 ? y : -INFINITY) : y;
 }
 
 // log(1 + x), x > -1: Goldberg's correction log(u) * x / (u - 1), u = 1 + x.
 __device__ __forceinline__ double flog1p(double x) {
+#pragma clang fp contract(off)
   const double u = 1.0 + x;
   const double um1 = u - 1.0;
   return um1 == 0.0 ? x : flog(u) * (x * rcp(um1));
@@ -170,6 +172,7 @@ struct LG3 {
 // record kernels keep the accurate form (MDFIT_TLOG_FIT off: no gain there).
 template <bool kTri = true, bool kTab = false>
 __device__ __forceinline__ LG3 lg3(double x) {
+#pragma clang fp contract(off)  // (every fusion explicit: the same bits in every inlined instance)
   constexpr double kHalfLog2Pi = 0.91893853320467274178;  // 0.5 ln(2 pi)
   double P = 1.0, dP = 0.0, d2P = 0.0;
   double xs = x;
@@ -198,7 +201,7 @@ __device__ __forceinline__ LG3 lg3(double x) {
   sl = fma(r2, -sl, 1.0 / 1260.0);
   sl = fma(r2, -sl, 1.0 / 360.0);
   sl = fma(r2, -sl, 1.0 / 12.0);
-  double L = fma(xs - 0.5, lx, -xs) + kHalfLog2Pi + r * sl;
+  double L = fma(r, sl, fma(xs - 0.5, lx, -xs) + kHalfLog2Pi);
   // psi(xs) ~ ln xs - r/2 - r2 (1/12 - r2 (1/120 - ...))
   double sp = fma(r2, -1.0 / 12.0, 691.0 / 32760.0);
   sp = fma(r2, -sp, 1.0 / 132.0);
@@ -206,7 +209,7 @@ __device__ __forceinline__ LG3 lg3(double x) {
   sp = fma(r2, -sp, 1.0 / 252.0);
   sp = fma(r2, -sp, 1.0 / 120.0);
   sp = fma(r2, -sp, 1.0 / 12.0);
-  double Ps = lx - 0.5 * r - r2 * sp;
+  double Ps = fma(-r2, sp, fma(-0.5, r, lx));
   // psi1(xs) ~ r + r2/2 + r^3 (1/6 - r2 (1/30 - ...))
   double Q = 0.0;
   if (kTri) {
@@ -216,7 +219,7 @@ __device__ __forceinline__ LG3 lg3(double x) {
     sq = fma(r2, -sq, 1.0 / 42.0);
     sq = fma(r2, -sq, 1.0 / 30.0);
     sq = fma(r2, -sq, 1.0 / 6.0);
-    Q = r + 0.5 * r2 + r * r2 * sq;
+    Q = fma(r * r2, sq, fma(0.5, r2, r));
   }
   if (shift) {
     const double iP = (MDFIT_RCP1 || kTab) ? rcp1(P) : rcp(P);
@@ -227,7 +230,7 @@ __device__ __forceinline__ LG3 lg3(double x) {
     L -= kTab ? flog_t<true>(P) : flog(P);
 #endif
     Ps -= s1;
-    if (kTri) Q += s1 * s1 - d2P * iP;  // sum 1/(x+j)^2
+    if (kTri) Q += fma(s1, s1, -(d2P * iP));  // sum 1/(x+j)^2
   }
   return {L, Ps, Q};
 }
@@ -238,6 +241,7 @@ __device__ __forceinline__ double lgam(double x) { return lg3<false>(x).l; }
 // Stirling remainder lnGamma(z) - [(z - 1/2) ln z - z + ln(2 pi)/2], z >= 10
 // (the series of lg3, O(z^-15))
 __device__ __forceinline__ double stirling_rem(double z) {
+#pragma clang fp contract(off)
   const double r = rcp(z), r2 = r * r;
   double sl = fma(r2, -1.0 / 156.0, 691.0 / 360360.0);
   sl = fma(r2, -sl, 1.0 / 1188.0);
@@ -257,6 +261,7 @@ __device__ __forceinline__ double stirling_rem(double z) {
 // (one ulp of lnGamma(1e9) is ~4e-6); the remainders' difference is tiny.
 // Below 10 the plain difference (small values, nothing to cancel).
 __device__ __forceinline__ double lgdiff(double z, double h) {
+#pragma clang fp contract(off)
   const double z1 = z + h;  // only for the branch test and the remainder
   if (z >= 10.0 && z1 >= 10.0) {
     const double t = flog1p(h * rcp(z));

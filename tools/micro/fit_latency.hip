@@ -9,7 +9,7 @@
 using namespace mdfit;
 
 template <int V>
-__global__ __launch_bounds__(64) void k(double* o, unsigned long long* cyc, int iters, double y0, double N0) {
+__global__ __launch_bounds__(64) void k(double* o, unsigned long long* cyc, int iters, double y0, double N0, int rt_pmd, int rt_accf) {
   const int lane = threadIdx.x;
   double u[4] = {-1.0 + 1e-3 * lane, -2.0, 0.01, 5.0};
   PointData pd;
@@ -17,7 +17,7 @@ __global__ __launch_bounds__(64) void k(double* o, unsigned long long* cyc, int 
   pd.N = (lane & 15) < 15 ? N0 + 7 * lane : 0.0;
   pd.k = (lane & 15) < 15 ? (lane & 15) : 0;
   pd.valid = (lane & 15) < 15;
-  pd.pmd = 1;
+  pd.pmd = V >= 7 ? rt_pmd : 1;
   double sink = 0.0;
   Theta th = make_theta<16>(true, u);
   double H[10] = {4, 0.1, 0.2, 0.3, 5, 0.1, 0.2, 6, 0.3, 7};
@@ -43,6 +43,16 @@ __global__ __launch_bounds__(64) void k(double* o, unsigned long long* cyc, int 
 #pragma unroll
       for (int j = 0; j < kNAcc; ++j) acc[j] = 0.0;
       point_accum<true>(pd, th, acc, 0);
+      double s = 0.0;
+#pragma unroll
+      for (int j = 0; j < kNAcc; ++j) s += acc[j];
+      u[0] += s * 1e-300;
+    } else if (V == 7) {
+      th = make_theta<16>(pd.pmd, u);
+      double acc[kNAcc];
+#pragma unroll
+      for (int j = 0; j < kNAcc; ++j) acc[j] = 0.0;
+      point_accum<true>(pd, th, acc, rt_accf);
       double s = 0.0;
 #pragma unroll
       for (int j = 0; j < kNAcc; ++j) s += acc[j];
@@ -81,20 +91,21 @@ int main() {
   unsigned long long* c;
   (void)hipMalloc(&o, 1024 * 64 * 8);
   (void)hipMalloc(&c, 1024 * 8);
-  const char* names[7] = {"make_theta", "point_accum (5 lg3 + contrib)", "make_theta + point_accum", "lg3 unshifted",
-                          "lg3 shifted", "newton_dir (PD)", "finish_eval + pgnorm + newton_dir"};
+  const char* names[8] = {"make_theta", "point_accum (5 lg3 + contrib)", "make_theta + point_accum", "lg3 unshifted",
+                          "lg3 shifted", "newton_dir (PD)", "finish_eval + pgnorm + newton_dir", "eval, runtime pmd / accf (0)"};
   for (int y0 = 0; y0 < 2; ++y0) {
     const double yy = y0 ? 500.0 : 3.0, NN = y0 ? 1e5 : 20.0;
-    for (int v = 0; v < 7; ++v) {
+    for (int v = 0; v < 8; ++v) {
       for (int blocks : {1, 1024}) {
         switch (v) {
-          case 0: k<0><<<blocks, 64>>>(o, c, 200, yy, NN); break;
-          case 1: k<1><<<blocks, 64>>>(o, c, 200, yy, NN); break;
-          case 2: k<2><<<blocks, 64>>>(o, c, 200, yy, NN); break;
-          case 3: k<3><<<blocks, 64>>>(o, c, 200, yy, NN); break;
-          case 4: k<4><<<blocks, 64>>>(o, c, 200, yy, NN); break;
-          case 5: k<5><<<blocks, 64>>>(o, c, 200, yy, NN); break;
-          case 6: k<6><<<blocks, 64>>>(o, c, 200, yy, NN); break;
+          case 0: k<0><<<blocks, 64>>>(o, c, 200, yy, NN, 1, 0); break;
+          case 1: k<1><<<blocks, 64>>>(o, c, 200, yy, NN, 1, 0); break;
+          case 2: k<2><<<blocks, 64>>>(o, c, 200, yy, NN, 1, 0); break;
+          case 3: k<3><<<blocks, 64>>>(o, c, 200, yy, NN, 1, 0); break;
+          case 4: k<4><<<blocks, 64>>>(o, c, 200, yy, NN, 1, 0); break;
+          case 5: k<5><<<blocks, 64>>>(o, c, 200, yy, NN, 1, 0); break;
+          case 6: k<6><<<blocks, 64>>>(o, c, 200, yy, NN, 1, 0); break;
+          case 7: k<7><<<blocks, 64>>>(o, c, 200, yy, NN, 1, 0); break;
         }
         unsigned long long h[1024];
         (void)hipDeviceSynchronize();
