@@ -489,10 +489,14 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
 #pragma unroll
     for (int j = 0; j < kNAcc; ++j) acc[j] = 0.0;
     const int accf = (esc & kEscPolish) != 0u;
-    // every slot of the wave fits model_null: a, b from the pads (point_accum)
-    const bool null_wave = !__any(pa.pmd != 0);
+    // every slot of the wave fits model_null: a, b from the pads; every slot
+    // holds an all-position fit: the two directions at the same |z| share a,
+    // b (point_accum: null_row, whole_pair)
+    // (slots not running evaluate garbage either way: they do not count)
+    const bool null_wave = !__any(running && pa.pmd != 0);
+    const bool whole_wave = !__any(running && !whole);
     if (PPL == 1) {
-      point_accum<true>(pa, th, acc, accf, null_wave);
+      point_accum<true>(pa, th, acc, accf, null_wave, whole_wave);
     } else {
       // lg3(phi) from a pad: lane 15's point b (all-position: both halves;
       // pair: the reverse half), lane 7's point b (pair: the forward half);
@@ -520,8 +524,10 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       const LG3 ta3 = lg3<true, MDFIT_TLOG_FIT>(pa.N + th.phi);
       const LG3 ta1 = lg3<true, MDFIT_TLOG_FIT>(pa.y + ga.a);
       const LG3 ta2 = lg3<true, MDFIT_TLOG_FIT>(pa.N - pa.y + ga.b);
-      LG3 ta4 = tb4, ta5 = tb5;  // (null: a, b are the half's; PMD: the point's own)
-      if (!null_wave) {
+      // (null: a, b are the half's; an all-position fit: point a is z = +k,
+      // point b z = -k, the same a, b; a pair: the point's own)
+      LG3 ta4 = tb4, ta5 = tb5;
+      if (!null_wave && !whole_wave) {
         ta4 = lg3<true, MDFIT_TLOG_FIT>(ga.a);
         ta5 = lg3<true, MDFIT_TLOG_FIT>(ga.b);
       }

@@ -86,6 +86,18 @@ __device__ __forceinline__ void logit_parts(double u, double& p, double& omp, do
   l1mp = pos ? -(u + sp) : -sp;
 }
 
+// The value of the lane 16 away (lane ^ 16): rows 0 <-> 1 and 2 <-> 3 of the
+// wave exchange, by v_permlane16_swap (gfx950; one swap per dword: with the
+// same register as both operands, the even rows' copy ends up in the odd rows
+// of the first result and the odd rows' in the even rows of the second).
+__device__ __forceinline__ double xrow(double v) {
+  const unsigned lo = (unsigned)__double2loint(v), hi = (unsigned)__double2hiint(v);
+  const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const bool odd = (threadIdx.x & 16) != 0;
+  return __hiloint2double((int)(odd ? rh[0] : rh[1]), (int)(odd ? rl[0] : rl[1]));
+}
+
 // Broadcast lane N of every 16-lane DPP row to the whole row (row_newbcast).
 template <int N>
 __device__ __forceinline__ double rowb(double v) {
@@ -278,9 +290,13 @@ __device__ __forceinline__ LG3 rowb3(const LG3& t) {
 // q phi and b = (1-q) phi are the same at every point of the row, and the pad
 // lane's lg3(y + a), lg3(N - y + b) ARE lg3(a), lg3(b), bitwise: broadcast
 // from it, 3 lg3 per point instead of 5.
+// whole_pair (wave-uniform; kRowPhi only): every 32-lane slot holds one
+// all-position fit, rows z > 0 and z < 0 at the same |z| lane by lane, so a
+// lane and its partner 16 away have the same a and b: the even row computes
+// lg3(a), the odd row lg3(b), and they exchange (xrow): 4 lg3 instead of 5.
 template <bool kRowPhi = false>
-__device__ __forceinline__ double point_accum(const PointData& pd, const Theta& th,
-                                              double acc[kNAcc], int accf = 0, bool null_row = false) {
+__device__ __forceinline__ double point_accum(const PointData& pd, const Theta& th, double acc[kNAcc],
+                                              int accf = 0, bool null_row = false, bool whole_pair = false) {
   const PointArgs pa = point_args(pd, th);
   const LG3 t3 = lg3<true, MDFIT_TLOG_FIT>(pd.N + th.phi);
   const LG3 t6 = kRowPhi ? rowb3<15>(t3) : lg3<true, MDFIT_TLOG_FIT>(th.phi);
@@ -290,6 +306,12 @@ __device__ __forceinline__ double point_accum(const PointData& pd, const Theta& 
   if (kRowPhi && null_row) {
     t4 = rowb3<15>(t1);
     t5 = rowb3<15>(t2);
+  } else if (kRowPhi && whole_pair) {
+    const bool odd = (threadIdx.x & 16) != 0;
+    const LG3 mine = lg3<true, MDFIT_TLOG_FIT>(odd ? pa.b : pa.a);
+    const LG3 other = {xrow(mine.l), xrow(mine.p), xrow(mine.q)};
+    t4 = odd ? other : mine;
+    t5 = odd ? mine : other;
   } else {
     t4 = lg3<true, MDFIT_TLOG_FIT>(pa.a);
     t5 = lg3<true, MDFIT_TLOG_FIT>(pa.b);

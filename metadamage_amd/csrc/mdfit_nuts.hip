@@ -1118,7 +1118,7 @@ struct PotC {
 // component-distributed: every lane resolves its own component (c < 3:
 // sigmoid, c == 3: exp), lanes 0-3 of the slot are broadcast.
 template <int PPL>
-__device__ __forceinline__ PotC potential_cd(const PointData pt[PPL], double x, bool whole) {
+__device__ __forceinline__ PotC potential_cd(const PointData pt[PPL], double x, bool whole, bool run = true) {
   constexpr int kG = PPL == 1 ? 16 : 8;
   const int c = (int)(threadIdx.x & 3);
   const bool hi8 = PPL == 2 && (threadIdx.x & 8);
@@ -1147,7 +1147,9 @@ __device__ __forceinline__ PotC potential_cd(const PointData pt[PPL], double x, 
   const double delta = bc(e, I3{}), v3 = bc(x, I3{});
   const double phi = delta + 2.0;
   const bool pmd = pt[0].pmd;
-  const bool null_wave = !__any(pmd);  // (PPL 1: the pad lanes then give lg3(a), lg3(b))
+  // (PPL 1; chains not running evaluate garbage either way and do not count)
+  const bool null_wave = !__any(run && pmd);      // the pad lanes give lg3(a), lg3(b)
+  const bool whole_wave = !__any(run && !whole);  // the two rows of a chain share a, b
   const double A = pmd ? A0 : 0.0, cc = pmd ? c0 : 0.0;
   double lprior = prq + v3 - delta * 1e-3;
   if (pmd) lprior += prA + prc;
@@ -1183,24 +1185,32 @@ __device__ __forceinline__ PotC potential_cd(const PointData pt[PPL], double x, 
     bad_lane = bad_lane || (pd.valid && !(D < 1.0));
     const double a = D * phi, b = (1.0 - D) * phi;
     const LG3 t1 = lg3<false, MDFIT_TLOG_NUTS>(pd.y + a);
-    LG3 t4;
+    const LG3 t2 = lg3<false, MDFIT_TLOG_NUTS>(pd.N - pd.y + b);
+    LG3 t4, t5;
     if (PPL == 1 && null_wave) {
       // every chain of the wave samples model_null: a = q phi is the row's, and
-      // the pad lane's lg3(0 + a) IS lg3(a), bitwise (likewise b below)
+      // the pad lane's lg3(0 + a) IS lg3(a), bitwise (likewise b)
       t4.l = rowb<15>(t1.l);
       t4.p = rowb<15>(t1.p);
-    } else {
-      t4 = lg3<false, MDFIT_TLOG_NUTS>(a);
-    }
-    const double la = t1.l - t4.l, Pa = t1.p - t4.p;
-    const LG3 t2 = lg3<false, MDFIT_TLOG_NUTS>(pd.N - pd.y + b);
-    LG3 t5;
-    if (PPL == 1 && null_wave) {
       t5.l = rowb<15>(t2.l);
       t5.p = rowb<15>(t2.p);
+    } else if (PPL == 1 && whole_wave) {
+      // every chain of the wave is an all-position chain: rows z > 0 and z < 0
+      // hold the same |z| lane by lane, so a lane and its partner 16 away share
+      // a, b -- the even row takes lg3(a), the odd row lg3(b), exchanged (xrow)
+      const bool odd = (threadIdx.x & 16) != 0;
+      const LG3 mine = lg3<false, MDFIT_TLOG_NUTS>(odd ? b : a);
+      LG3 other;
+      other.l = xrow(mine.l);
+      other.p = xrow(mine.p);
+      other.q = 0.0;
+      t4 = odd ? other : mine;
+      t5 = odd ? mine : other;
     } else {
+      t4 = lg3<false, MDFIT_TLOG_NUTS>(a);
       t5 = lg3<false, MDFIT_TLOG_NUTS>(b);
     }
+    const double la = t1.l - t4.l, Pa = t1.p - t4.p;
     const double lb = t2.l - t5.l, Pb = t2.p - t5.p;
     const LG3 t3 = (PPL == 1 || pi == 1) ? t3b : lg3<false, MDFIT_TLOG_NUTS>(pd.N + phi);
     const double ell = (la + lb) - (t3.l - t6l);
@@ -1533,7 +1543,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
     PotC P = potential_cd<PPL>(pd, zev, whole);
     P.U += 0.0 * P0.U * (double)(it > (1 << 30));
 #else
-    const PotC P = potential_cd<PPL>(pd, zev, whole);
+    const PotC P = potential_cd<PPL>(pd, zev, whole, running);
 #endif
     NSTAMP(2);
     if (!running) continue;
