@@ -73,6 +73,10 @@ constexpr double kLX = 2.5;
 #define MDFIT_HPDI_STOP 16.0
 #endif
 constexpr double kStop = MDFIT_HPDI_STOP;  // counts: the exact fix-up walk finishes
+#ifndef MDFIT_HPDI_ROOT_TOL
+#define MDFIT_HPDI_ROOT_TOL 0.05
+#endif
+constexpr double kRootTol = MDFIT_HPDI_ROOT_TOL;  // counts: a window end's Newton root is settled
 constexpr double kGLX[3] = {0.2386191860831969, 0.6612093864662645, 0.9324695142031521};
 constexpr double kGLW[3] = {0.4679139345726910, 0.3607615730481386, 0.1713244923791704};
 
@@ -574,7 +578,7 @@ __device__ __forceinline__ bool wide_iter(Wide& W) {
         else rhi = xr;
         double xn = sx != 0.0 ? xr - gx / sx : 0.5 * (rlo + rhi);
         if (!(rlo < xn && xn < rhi)) xn = 0.5 * (rlo + rhi);
-        const bool conv = fabs(xn - xr) < 0.05;
+        const bool conv = fabs(xn - xr) < kRootTol;
         xr = xn;
         fin = conv || ++k >= 60;
       }
@@ -610,7 +614,7 @@ __device__ __forceinline__ bool wide_iter(Wide& W) {
         else rhi = xr;
         double xn = sx != 0.0 ? xr - gx / sx : 0.5 * (rlo + rhi);
         if (!(rlo < xn && xn < rhi)) xn = 0.5 * (rlo + rhi);
-        const bool conv = fabs(xn - xr) < 0.05;
+        const bool conv = fabs(xn - xr) < kRootTol;
         xr = xn;
         if (conv) break;
       }
