@@ -198,7 +198,7 @@ int mdfit_special(const double* x, int64_t n, double* out3, void* hip_stream);
 int mdfit_poison_lds(void* hip_stream);
 
 /*
- * MAP predictive HPDI (MDFIT-HPDI v1): the 68 % highest-
+ * MAP predictive HPDI (MDFIT-HPDI v2): the 68 % highest-
  * probability window [lo, hi] (integer counts, returned as double) of
  * BetaBinomial(alpha, beta, N), the population form of numpyro's
  * hpdi(obs/N, 0.68) over predictive draws (fits.py:112-120, 260-261).  The

@@ -14,7 +14,7 @@
 //                              the 6 modes, n_sigma x3, asymmetry, predictive
 //                              medians, sums, noise (fits.py:230-376)
 //   K4 hpdi_kernel     one lane per (taxon, position): the 68 % predictive
-//                      HPDI of the PMD-all mode (MDFIT-HPDI v1, mdfit_hpdi.h;
+//                      HPDI of the PMD-all mode (MDFIT-HPDI v2, mdfit_hpdi.h;
 //                      fits.py:112-120, 260-261)
 //
 // K1 work decomposition (details at fit_kernel): lane = position; a "slot"
@@ -809,7 +809,7 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
           // the PMD-all fit just ended: publish its (q, A, c, phi) -- make_theta's
           // arithmetic, NaN for invalid input -- as the next entry of the ready
           // list that hpdi_stream_kernel consumes beside this kernel (the
-          // predictive HPDI, MDFIT-HPDI v1).  The slot's first lane writes the
+          // predictive HPDI, MDFIT-HPDI v2).  The slot's first lane writes the
           // entry's five fields as relaxed agent-scope atomic stores of their
           // bit complements (ready_put): K0 zeroed the list, so a field reads
           // non-zero exactly once this call has written it, and a reader takes
@@ -1068,7 +1068,7 @@ __global__ __launch_bounds__(kWave) void assemble_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// K4: 68 % predictive HPDI (MDFIT-HPDI v1, mdfit_hpdi.h) of the PMD-all mode at
+// K4: 68 % predictive HPDI (MDFIT-HPDI v2, mdfit_hpdi.h) of the PMD-all mode at
 // every position (fits.py:112-120, 260-261).  K4a: one lane per (taxon,
 // position) -- neighbouring lanes hold neighbouring positions of one taxon;
 // windows of sd <= 100 points are finished there (the greedy), wide ones go to

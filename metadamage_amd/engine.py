@@ -324,7 +324,7 @@ def betabinom_logpmf(y, N, a, b, device="cuda"):
 
 def hpdi68(N, a, b, device="cuda"):
     """68 % predictive window [lo, hi] of BetaBinomial(a, b, N) on the device
-    (MDFIT-HPDI v1, mdfit_hpdi68; parity tests)."""
+    (MDFIT-HPDI v2, mdfit_hpdi68; parity tests)."""
     torch = _torch()
     lib = _lib.load()
     shape = np.broadcast(N, a, b).shape

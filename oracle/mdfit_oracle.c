@@ -815,7 +815,7 @@ static void noise(const uint32_t* mm, double out3[3]) {
 
 /* MAP predictive summary at point i (fits.py:112-120 with the mode as the one
  * posterior sample): median := D(z); HPDI := the 68 % window [lo, hi] / N of
- * BetaBinomial(D phi, (1-D) phi, N) (MDFIT-HPDI v1, mdfit_hpdi.c); NaN when
+ * BetaBinomial(D phi, (1-D) phi, N) (MDFIT-HPDI v2, mdfit_hpdi.c); NaN when
  * N = 0 (the reference divides 0 draws by N = 0, fits.py:115).  want_hpdi = 0:
  * the median only (D_max_forward / _reverse). */
 /* tests may switch the HPDI off (oracle_set_hpdi(0)) to check the other

@@ -1,4 +1,4 @@
-"""Golden vectors for the MAP predictive HPDI (MDFIT-HPDI v1), from scipy.
+"""Golden vectors for the MAP predictive HPDI (MDFIT-HPDI v2), from scipy.
 
     python tests/golden/make_golden_hpdi.py      # writes tests/golden/hpdi_golden.npz
 

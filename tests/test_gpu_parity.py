@@ -111,7 +111,7 @@ def oracle_lib_init(oracle_lib, model, subset, y30, N30):
 
 
 # --------------------------------------------------------------------------
-# MAP predictive HPDI (MDFIT-HPDI v1): the kernel's window vs scipy and the oracle
+# MAP predictive HPDI (MDFIT-HPDI v2): the kernel's window vs scipy and the oracle
 # --------------------------------------------------------------------------
 def test_hpdi_kernel_vs_scipy_and_oracle(engine, oracle_lib):
     from pathlib import Path

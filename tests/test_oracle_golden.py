@@ -177,7 +177,7 @@ def test_packing_vs_group_to_numpyro_data(ref_golden):
 
 
 # --------------------------------------------------------------------------
-# MAP predictive HPDI (MDFIT-HPDI v1, oracle/mdfit_hpdi.c)
+# MAP predictive HPDI (MDFIT-HPDI v2, oracle/mdfit_hpdi.c)
 # --------------------------------------------------------------------------
 def _window_rel(lo, hi, rlo, rhi):
     """relative error of the reported bounds lo/N, hi/N (counts >= 1 as scale)"""
