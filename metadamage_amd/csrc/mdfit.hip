@@ -250,12 +250,20 @@ __device__ __forceinline__ void hpdi_write(const HpdiIO& io, int64_t item, doubl
 // the two-list buffer that K4b drains longest-first: windows whose mode lies
 // within 1.5 tau of a support end (log-variable panels, support-end walks,
 // one-sided windows: ~2.5 level iterations) from the front (count ctr[0]), the
-// clean two-sided ones (~1.45) from the back (count ctr[2]).  Wave-collective
-// over the active lanes (the first one does the list atomics).
+// clean two-sided ones (~1.45) from the back (count ctr[2]).  Block-collective
+// (kPrepBlock threads, every thread calls): one atomic per list per block --
+// per wave, the two list counters were 117k same-address atomics at 125k taxa.
+#ifndef MDFIT_PREP_BLOCK
+#define MDFIT_PREP_BLOCK 256
+#endif
+constexpr int kPrepBlock = MDFIT_PREP_BLOCK;
 template <bool kFit>
 __device__ __forceinline__ void hpdi_position(const HpdiIO& io, int64_t item, bool valid, bool skip, double N, double a,
                                               double b, int64_t n_items, int* __restrict__ ctr,
                                               hpdi::WideRec* __restrict__ recs) {
+  constexpr int kW = kPrepBlock / kWave;
+  __shared__ int s_n[2][kW];
+  __shared__ int s_b[2];
   bool wide = false;
   hpdi::WideRec rec;
   if (valid) {
@@ -268,19 +276,32 @@ __device__ __forceinline__ void hpdi_position(const HpdiIO& io, int64_t item, bo
     const double tau = sqrt(rec.sd * rec.sd + (rec.mu - rec.m) * (rec.mu - rec.m));
     near = rec.m < 1.5 * tau || rec.N - rec.m < 1.5 * tau;
   }
-  const int first = __ffsll((unsigned long long)__ballot(1)) - 1;
+  const int w = (int)threadIdx.x / kWave, ln = (int)threadIdx.x % kWave;
   const unsigned long long mf = __ballot(wide && near), mb = __ballot(wide && !near);
-  if ((mf | mb) == 0ull) return;
-  int bf = 0, bb = 0;
-  if ((int)threadIdx.x == first) {
-    if (mf) bf = atomicAdd(ctr, __popcll(mf));
-    if (mb) bb = atomicAdd(ctr + 2, __popcll(mb));
+  if (ln == 0) {
+    s_n[0][w] = __popcll(mf);
+    s_n[1][w] = __popcll(mb);
   }
-  bf = __shfl(bf, first);
-  bb = __shfl(bb, first);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tf = 0, tb = 0;
+#pragma unroll
+    for (int k = 0; k < kW; ++k) {
+      tf += s_n[0][k];
+      tb += s_n[1][k];
+    }
+    s_b[0] = tf ? atomicAdd(ctr, tf) : 0;
+    s_b[1] = tb ? atomicAdd(ctr + 2, tb) : 0;
+  }
+  __syncthreads();
   if (wide) {
+    int bf = s_b[0], bb = s_b[1];
+    for (int k = 0; k < w; ++k) {
+      bf += s_n[0][k];
+      bb += s_n[1][k];
+    }
     rec.item = item;
-    const unsigned long long below = (1ull << threadIdx.x) - 1ull;
+    const unsigned long long below = (1ull << ln) - 1ull;
     const int64_t slot = near ? (int64_t)(bf + __popcll(mf & below)) : n_items - 1 - (bb + __popcll(mb & below));
     recs[slot] = rec;
   }
@@ -1079,9 +1100,9 @@ __global__ __launch_bounds__(kWave) void assemble_kernel(
 // (mdfit_hpdi68, parity tests).
 // ---------------------------------------------------------------------------
 template <bool kFit>
-__global__ __launch_bounds__(kWave) void hpdi_prep_kernel(HpdiIO io, int64_t n_items, int* __restrict__ ctr,
-                                                          hpdi::WideRec* __restrict__ recs) {
-  const int64_t item = (int64_t)blockIdx.x * kWave + threadIdx.x;
+__global__ __launch_bounds__(kPrepBlock) void hpdi_prep_kernel(HpdiIO io, int64_t n_items, int* __restrict__ ctr,
+                                                               hpdi::WideRec* __restrict__ recs) {
+  const int64_t item = (int64_t)blockIdx.x * kPrepBlock + threadIdx.x;
   const bool valid = item < n_items;
   double N = 0.0, a = 0.0, b = 0.0;
   bool skip = true;
@@ -1224,7 +1245,7 @@ __device__ __noinline__ bool defer_items(int* ws, int* defer, bool pending, int 
 }
 
 #ifndef MDFIT_STREAM_WAVES_PER_CU
-#define MDFIT_STREAM_WAVES_PER_CU 4  // A/B at 10k and 125k taxa (tools/overlap_exp.py): 4 with the fit waves' base priority 1
+#define MDFIT_STREAM_WAVES_PER_CU 3  // A/B at 10k taxa (tools/_gpu_r05b.sh, profiles/r05_stream_waves.txt): 3 since HPDI v2 (1.08 ms; 4: 1.12, 2: 1.26); round 4: 4
 #endif
 template <bool kEarly>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPDI_WAVES_PER_EU))) void hpdi_stream_kernel(
@@ -1666,8 +1687,9 @@ int launch_hpdi(const mdfit::HpdiIO& io, int64_t n_items, int* ctr, mdfit::hpdi:
   if (n_items == 0) return 0;
   if (prep) {
     mdfit::host::debug_poison(s);
-    hipLaunchKernelGGL(mdfit::hpdi_prep_kernel<kFit>, dim3((unsigned)((n_items + mdfit::kWave - 1) / mdfit::kWave)),
-                       dim3(mdfit::kWave), 0, s, io, n_items, ctr, recs);
+    hipLaunchKernelGGL(mdfit::hpdi_prep_kernel<kFit>,
+                       dim3((unsigned)((n_items + mdfit::kPrepBlock - 1) / mdfit::kPrepBlock)), dim3(mdfit::kPrepBlock),
+                       0, s, io, n_items, ctr, recs);
     if (int rc = check_launch("hpdi_prep_kernel")) return rc;
   }
   // no more waves than are resident, and no more than the items need (the
