@@ -12,14 +12,14 @@ OUT=gpurun_out/prof
 rm -rf "$OUT" && mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
-    python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-c4-base > "$OUT/bench_trace.json" 2> "$OUT/trace.err" && \
+    python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-c4-base --no-c3 > "$OUT/bench_trace.json" 2> "$OUT/trace.err" && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-c4-base > /dev/null 2> "$OUT/fetch.err" && \
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-c4-base --no-c3 > /dev/null 2> "$OUT/fetch.err" && \
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-c4-base > /dev/null 2> "$OUT/write.err" && \
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-c4-base --no-c3 > /dev/null 2> "$OUT/write.err" && \
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU \
     SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES -d "$OUT/sq" -o run --output-format csv -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-c4-base > /dev/null 2> "$OUT/sq.err" && \
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-c4-base --no-c3 > /dev/null 2> "$OUT/sq.err" && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/nuts_trace" -o run --output-format csv -- \
     python3 bench.py --mode nuts --no-cpu-baseline > "$OUT/bench_nuts_trace.json" 2> "$OUT/nuts_trace.err" && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/nuts_fetch" -o run --output-format csv -- \
