@@ -305,7 +305,13 @@ int mdi_open(const char* path, int n_threads, mdi_table** out) {
   mdi_table* t = new mdi_table();
   t->size = (size_t)sb.st_size;
   if (t->size > 0) {
-    t->map = mmap(nullptr, t->size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+    // (no MAP_POPULATE: the row count below faults the pages in on every
+    // thread at once -- populating them here took ~13 ms on one thread)
+    static const bool populate = [] {
+      const char* e = std::getenv("MDI_POPULATE");
+      return e != nullptr && std::atoi(e) != 0;
+    }();
+    t->map = mmap(nullptr, t->size, PROT_READ, MAP_PRIVATE | (populate ? MAP_POPULATE : 0), fd, 0);
     if (t->map == MAP_FAILED) {
       close(fd);
       delete t;
@@ -440,16 +446,16 @@ int mdi_strings(const mdi_table* t, int which, char* buf, int64_t* offsets) {
 
 void mdi_free(mdi_table* t) {
   if (!t) return;
-  // unmapping a populated 300 MB mapping takes ~20 ms of page-table
-  // teardown: done on a detached thread (nothing views the mapping any more:
-  // the string tables were copied out by mdi_parse_into)
-  if (t->map && t->map != MAP_FAILED) {
-    void* m = t->map;
-    const size_t n = t->size;
-    if (n >= ((size_t)1 << 24)) std::thread([m, n] { munmap(m, n); }).detach();
-    else munmap(m, n);
-  }
-  delete t;
+  // unmapping a populated 300 MB mapping takes ~20 ms of page-table teardown,
+  // and the chunks' string tables (~1e5 hash nodes and strings per file) ~8 ms
+  // of frees: both on a detached thread (nothing views the mapping or the
+  // tables any more: the caller copied the strings out with mdi_strings)
+  auto release = [](mdi_table* x) {
+    if (x->map && x->map != MAP_FAILED) munmap(x->map, x->size);
+    delete x;
+  };
+  if (t->size >= ((size_t)1 << 24)) std::thread(release, t).detach();
+  else release(t);
 }
 
 const char* mdi_last_error(void) { return g_err; }
