@@ -1099,6 +1099,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PPL == 1 
 #ifndef MDFIT_NUTS_CD
 #define MDFIT_NUTS_CD 1
 #endif
+#ifndef MDFIT_NUTS_STEAL
+#define MDFIT_NUTS_STEAL 1  // chain waves take tasks from the other XCDs' queues once theirs runs dry
+#endif
 #ifndef MDFIT_NUTS_CD_WAVES
 #define MDFIT_NUTS_CD_WAVES 4  // 128 VGPRs, no spill with MachineLICM off (build_hip)
 #endif
@@ -1346,8 +1349,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   ColdState& C = scold[row];                                                              \
   (void)h, (void)c, (void)row16, (void)leader, (void)V, (void)C
   MDFIT_CD_LAYOUT(threadIdx.x);
-  const int qi = blockIdx.x % kQueues;
-  const int64_t tl = T * qi / kQueues, nq = T * (qi + 1) / kQueues - tl;
+  // a wave serves its XCD's queue, then (MDFIT_NUTS_STEAL) the next queues in
+  // turn once that one runs dry: the chains are ~1e4 trips long, so the last
+  // ones started decide the kernel's end (which wave runs a chain changes no
+  // draw: the streams are keyed by taxon and sub-fit)
+  int qi = blockIdx.x % kQueues, qs = 0;
+  int64_t tl = T * qi / kQueues, nq = T * (qi + 1) / kQueues - tl;
   const int W = o.num_warmup, S = o.num_samples;
 
   // the lane's points: counts kept as integers across the loop (converted at
@@ -1453,11 +1460,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       const unsigned long long m = __ballot(need && r == 0);
       int base = 0;
       if (lane == 0) base = atomicAdd(ws + qi, __popcll(m));
-      base = __shfl(base, 0);
+      base = __builtin_amdgcn_readfirstlane(base);
+      const bool dry = (int64_t)base + __popcll(m) > 4 * nq;  // wave-uniform
       if (need) {
         const int64_t task = (int64_t)base + __popcll(m & ((1ull << leader) - 1ull));
         if (task >= 4 * nq) {
-          drained = 1;
+          drained = !MDFIT_NUTS_STEAL || qs + 1 >= kQueues ? 1 : 0;  // (else: the next queue next trip)
           mode = 0;
         } else {
           const int kind = (int)(task / nq);
@@ -1466,6 +1474,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
           C.sub = kind == 0 ? 0 : (kind == 2 ? 1 : (kind == 1 ? 2 : 4) + h);
           starting = true;
         }
+      }
+      if (MDFIT_NUTS_STEAL && dry && qs + 1 < kQueues) {
+        ++qs;
+        qi = (qi + 1) % kQueues;
+        tl = T * qi / kQueues;
+        nq = T * (qi + 1) / kQueues - tl;
       }
     }
     if (starting) {
