@@ -1099,6 +1099,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PPL == 1 
 #ifndef MDFIT_NUTS_CD
 #define MDFIT_NUTS_CD 1
 #endif
+#ifndef MDFIT_POST_U32
+#define MDFIT_POST_U32 1  // post kernel: the draws' counts sorted (4 B each) and a one-pass WAIC: 4 KB of LDS instead of 8
+#endif
 #ifndef MDFIT_NUTS_STEAL
 #define MDFIT_NUTS_STEAL 1  // chain waves take tasks from the other XCDs' queues once theirs runs dry
 #endif
@@ -1985,6 +1988,15 @@ __device__ double predictive_frac(const Stream& st, int s, int col, int k, doubl
   return binomial_draw(d, Nn, p) / Nn;
 }
 
+// the draw itself (an integer count <= N): predictive_frac = predictive_count / N
+__device__ uint32_t predictive_count(const Stream& st, int s, int col, int k, double Nn, const double* th) {
+  const double D = d_at(th, true, k);
+  Draw d{&st, 0xFFFD0000u + (uint32_t)s, (uint32_t)col << 16};
+  const double lx = log_gamma_draw(d, D * th[3]), ly = log_gamma_draw(d, (1.0 - D) * th[3]);
+  const double p = 1.0 / (1.0 + exp(ly - lx));
+  return (uint32_t)binomial_draw(d, Nn, p);
+}
+
 // wave-wide reductions
 __device__ __forceinline__ double wsum(double v) { return gsum<64>(v); }
 __device__ __forceinline__ double wmax(double v) {
@@ -2017,6 +2029,57 @@ __device__ void lds_sort(double* v, int n) {
 }
 
 // np.median + numpyro hpdi(prob 0.68) of the S sorted values
+// bitonic sort of n counts in LDS (padded to a power of two with UINT32_MAX)
+__device__ void lds_sort_u32(uint32_t* v, int n) {
+  int m = 1;
+  while (m < n) m <<= 1;
+  for (int j = n + threadIdx.x; j < m; j += kWave) v[j] = 0xFFFFFFFFu;
+  __syncthreads();
+  for (int k = 2; k <= m; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int x = threadIdx.x; x < m; x += kWave) {
+        const int y = x ^ j;
+        if (y > x) {
+          const uint32_t a = v[x], b = v[y];
+          const bool up = (x & k) == 0;
+          if ((a > b) == up) {
+            v[x] = b;
+            v[y] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+// median_hpdi over the fractions c / N of sorted counts c: each fraction is
+// formed as predictive_frac forms it, so the result is median_hpdi's on the
+// sorted fractions bit for bit (c -> c / N is monotone: the same order, ties
+// where the fractions tie)
+__device__ void median_hpdi_counts(const uint32_t* c, int S, double Nn, double out3[3]) {
+  auto f = [&](int x) { return (double)c[x] / Nn; };
+  out3[0] = (S & 1) ? f(S / 2) : 0.5 * (f(S / 2 - 1) + f(S / 2));
+  const int len = (int)(0.68 * S);
+  double bw = INFINITY;
+  int best = 0;
+  for (int x = threadIdx.x; x < S - len; x += kWave) {
+    const double w = f(x + len) - f(x);
+    if (w < bw) {  // first minimum per lane
+      bw = w;
+      best = x;
+    }
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    const double ow = __shfl_xor(bw, o, 64);
+    const int ob = __shfl_xor(best, o, 64);
+    if (ow < bw || (ow == bw && ob < best)) {
+      bw = ow;
+      best = ob;
+    }
+  }
+  out3[1] = f(best);
+  out3[2] = f(best + len);
+}
 __device__ void median_hpdi(const double* v, int S, double out3[3]) {
   out3[0] = (S & 1) ? v[S / 2] : 0.5 * (v[S / 2 - 1] + v[S / 2]);
   const int len = (int)(0.68 * S);
@@ -2058,6 +2121,7 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
   // fixed kMaxSamples array made the block 37 KB and capped the kernel at one
   // wave per SIMD)
   extern __shared__ double s_v[];
+  uint32_t* s_c = reinterpret_cast<uint32_t*>(s_v);  // (MDFIT_POST_U32: the predictive draws' counts)
   const int lane = threadIdx.x;
   const int64_t t = blockIdx.x;
   const int S = o.num_samples;
@@ -2118,6 +2182,34 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
       const double yy = s_y[col], nn = s_N[col];
       const int k = col < kNHalf ? col : col - kNHalf;
       const double lc = lg3<false, MDFIT_TLOG_NUTS>(nn + 1.0).l - lg3<false, MDFIT_TLOG_NUTS>(yy + 1.0).l - lg3<false, MDFIT_TLOG_NUTS>(nn - yy + 1.0).l;
+#if MDFIT_POST_U32
+      // one pass: per lane a running max with its sum of exp (log-sum-exp) and
+      // Welford's mean / M2 over its draws, combined across the wave -- the
+      // lppd and variance of the two passes, to rounding, with no per-draw store
+      double mxl = -INFINITY, sel = 0.0, mul = 0.0, m2l = 0.0, cnt = 0.0;
+      for (int x = lane; x < S; x += kWave) {
+        const double* th = smp + ((int64_t)s * S + x) * 4;
+        const double D = d_at(th, pmd, k), phi = th[3];
+        const double a = D * phi, b = (1.0 - D) * phi;
+        const double lp = lc + (lg3<false, MDFIT_TLOG_NUTS>(yy + a).l - lg3<false, MDFIT_TLOG_NUTS>(a).l) + (lg3<false, MDFIT_TLOG_NUTS>(nn - yy + b).l - lg3<false, MDFIT_TLOG_NUTS>(b).l) -
+                          (lg3<false, MDFIT_TLOG_NUTS>(nn + phi).l - lg3<false, MDFIT_TLOG_NUTS>(a + b).l);
+        if (lp > mxl) {
+          sel = sel * exp(mxl - lp) + 1.0;
+          mxl = lp;
+        } else {
+          sel += exp(lp - mxl);
+        }
+        cnt += 1.0;
+        const double dlt = lp - mul;
+        mul += dlt / cnt;
+        m2l = fma(dlt, lp - mul, m2l);
+      }
+      const double mx = wmax(mxl);
+      const double se = wsum(cnt > 0.0 ? sel * exp(mxl - mx) : 0.0);
+      const double mean = wsum(cnt * mul) / S;
+      const double dm = mul - mean;
+      const double var = wsum(m2l + cnt * dm * dm) / S;
+#else
       double mx = -INFINITY, sm = 0.0;
       for (int x = lane; x < S; x += kWave) {
         const double* th = smp + ((int64_t)s * S + x) * 4;
@@ -2138,6 +2230,7 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
       }
       se = wsum(se);
       var = wsum(var) / S;
+#endif
       const double lppd = mx + log(se) - log((double)S);
       if (lane == 0) s_waic[s][col] = -2.0 * (lppd - var);
       __syncthreads();
@@ -2210,14 +2303,25 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
       const Stream st = make_stream(o.seed, o.index_base + t, s);
 #ifdef MDFIT_DEV_POST_NODRAW
       for (int x = lane; x < S; x += kWave) s_v[x] = smp[((int64_t)s * S + x) * 4] * (double)(col + 1);
+      (void)s_c;
+#else
+#if MDFIT_POST_U32
+      for (int x = lane; x < S; x += kWave)
+        s_c[x] = predictive_count(st, x, col, k, nn, smp + ((int64_t)s * S + x) * 4);
 #else
       for (int x = lane; x < S; x += kWave) s_v[x] = predictive_frac(st, x, col, k, nn, smp + ((int64_t)s * S + x) * 4);
 #endif
+#endif
       __syncthreads();
+#if MDFIT_POST_U32
+      lds_sort_u32(s_c, S);
+      median_hpdi_counts(s_c, S, nn, m3);
+#else
 #ifndef MDFIT_DEV_POST_NOSORT
       lds_sort(s_v, S);
 #endif
       median_hpdi(s_v, S, m3);
+#endif
       __syncthreads();
     }
     if (lane == 0) {
@@ -2378,8 +2482,9 @@ int fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t 
   hipLaunchKernelGGL(chain, dim3((unsigned)g), dim3(kWave), 0, s, y, N, n_taxa, o, out, ws, samples);
   if (int rc = host::check_launch("nuts_chain_kernel")) return rc;
   host::prof_mark(2, s);
-  size_t sv_bytes = sizeof(double);
-  while (sv_bytes < (size_t)o.num_samples * sizeof(double)) sv_bytes <<= 1;  // lds_sort pads to 2^k
+  const size_t elt = MDFIT_POST_U32 ? sizeof(uint32_t) : sizeof(double);
+  size_t sv_bytes = elt;
+  while (sv_bytes < (size_t)o.num_samples * elt) sv_bytes <<= 1;  // the sort pads to 2^k
   host::debug_poison(s);
   hipLaunchKernelGGL(nuts_post_kernel, dim3((unsigned)n_taxa), dim3(kWave), sv_bytes, s, y, N, mm, n_taxa, o,
                      samples, out, pred, status);
