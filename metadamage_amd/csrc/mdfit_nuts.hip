@@ -124,6 +124,12 @@ double normal(const Stream& s, uint32_t w2, uint32_t w3) {
   const double u1 = 1.0 - u53(o.x, o.y), u2 = u53(o.z, o.w);
   return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
 }
+// the same, inlined (the post kernel's draws: no call per normal)
+__device__ __forceinline__ double normal_inl(const Stream& s, uint32_t w2, uint32_t w3) {
+  const uint4 o = block(s, w2, w3);
+  const double u1 = 1.0 - u53(o.x, o.y), u2 = u53(o.z, o.w);
+  return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+}
 
 __device__ __forceinline__ double sel4(const double v[4], int j) {
   return j == 0 ? v[0] : (j == 1 ? v[1] : (j == 2 ? v[2] : v[3]));
@@ -1099,6 +1105,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PPL == 1 
 #ifndef MDFIT_NUTS_CD
 #define MDFIT_NUTS_CD 1
 #endif
+#ifndef MDFIT_POST_NRM_INLINE
+#define MDFIT_POST_NRM_INLINE 1  // the post kernel's gamma draws call an inlined normal
+#endif
 #ifndef MDFIT_POST_U32
 #define MDFIT_POST_U32 1  // post kernel: the draws' counts sorted (4 B each) and a one-pass WAIC: 4 KB of LDS instead of 8
 #endif
@@ -1911,7 +1920,7 @@ struct Draw {
   const Stream* st;
   uint32_t w2, w3;
   __device__ double uni() { return uniform(*st, w2, w3++); }
-  __device__ double nrm() { return normal(*st, w2, w3++); }
+  __device__ double nrm() { return MDFIT_POST_NRM_INLINE ? normal_inl(*st, w2, w3++) : normal(*st, w2, w3++); }
 };
 
 __device__ double log_gamma_draw(Draw& d, double alpha) {
