@@ -441,7 +441,7 @@ def main():
             line["cpu_baseline"], ref = cpu_baseline(b, cores, visible)
             if ref_dispatch is not None:
                 line["cpu_baseline"]["reference_dispatch"] = ref_dispatch
-            line["parity"] = parity(o, st, *ref[::2], kind="bitwise-algorithm (same MDFIT-MAP v1 as the oracle)")
+            line["parity"] = parity(o, st, *ref[::2], kind="bitwise-algorithm (same MDFIT-MAP v1.1 as the oracle)")
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -4,7 +4,7 @@ seed 3) against the CPU oracle on all 25 result columns, with bench.py's
 metric (|gpu - cpu| / max(|cpu|, 1e-2) over taxa both fitted) and the status
 agreement, as one JSON line per size.
 
-    python tools/parity_at_scale.py > profiles/r01_parity_at_scale.jsonl
+    python tools/parity_at_scale.py > profiles/rNN_parity_at_scale.jsonl
     python tools/parity_at_scale.py --sizes 1000000:4   # C4's whole 1M taxa on one GPU
 """
 
@@ -60,7 +60,7 @@ def main() -> None:
             print(f"oracle {hi}/{T} taxa, {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
         ref, rpred, rst = (np.concatenate([q[i] for q in parts]) for i in range(3))
         cpu_s = time.perf_counter() - t0
-        line = parity(out, st, ref, rst, kind="MAP, same MDFIT-MAP v1 as the oracle")
+        line = parity(out, st, ref, rst, kind="MAP, same MDFIT-MAP v1.1 + MDFIT-HPDI v2 as the oracle")
         line.update(config=label, n_taxa=T, seed=seed, gpu_status_ok=float((st == 0).mean()),
                     cpu_status_ok=float((rst == 0).mean()),
                     status_mismatch_tax_index=[int(i) for i in np.nonzero(st != rst)[0][:10]],
