@@ -11,6 +11,13 @@ Two measurements:
     last parquet written (max over ranks), reported as taxa fitted per second.
 
     python tools/c5_pipeline.py --files 10 --taxa 100000 --inference map
+    python tools/c5_pipeline.py --stages 0 --check   # + every file's frames vs the oracle
+
+--check (MAP, after the timed run, outside it): each file's counts parquet is
+packed again and fitted by the CPU oracle (oracle/, the checker only); the
+driver's written result frame must keep exactly the oracle's status-0 taxa, and
+every result column is compared (the frames store float32) with bench.py's
+metric |gpu - cpu| / max(|cpu|, 1e-2).
 """
 
 from __future__ import annotations
@@ -126,6 +133,44 @@ def _trace_summary(events, t_start, wall):
                          sorted(events, key=lambda e: e[2])]}
 
 
+def check(files, out_dir, inference, threads=16):
+    """The full-size C5 run against the oracle, one JSON line per file."""
+    import numpy as np
+
+    from metadamage_amd import _lib, fits, io
+    from oracle.oracle import OracleLib
+
+    oracle = OracleLib()
+    for f in files:
+        cfg = _cfg(out_dir, inference)
+        cfg.add_filename(f)
+        dfr = io.Parquet(cfg.filename_fit_results).load()
+        p = fits.pack_counts(io.Parquet(cfg.filename_counts).load(), cfg)
+        t0 = time.perf_counter()
+        ref, _, rst = oracle.fit_batch(p.y, p.N, p.mm, threads=threads)
+        cpu_s = time.perf_counter() - t0
+        keep = rst == _lib.OK
+        tids = np.asarray(p.tax_id, dtype=np.int64)
+        got = dfr.set_index(dfr["tax_id"].astype(np.int64))
+        same_set = bool(len(got) == keep.sum() and np.array_equal(np.sort(got.index.to_numpy()), np.sort(tids[keep])))
+        rows = {t: i for i, t in enumerate(tids)}
+        common = tids[keep]
+        ri = np.array([rows[t] for t in common], dtype=np.int64)
+        worst, per = 0.0, {}
+        for j, name in enumerate(_lib.RESULT_FIELDS):
+            a = got.loc[common, name].to_numpy(np.float64)
+            r = ref[ri, j].astype(np.float32).astype(np.float64)
+            rel = np.abs(a - r) / np.maximum(np.abs(r), 1e-2)
+            rel = np.where(np.isnan(a) & np.isnan(r), 0.0, rel)
+            per[name] = float(np.nan_to_num(rel, nan=np.inf).max()) if rel.size else 0.0
+            worst = max(worst, per[name])
+        wf = max(per, key=per.get) if per else None
+        print(json.dumps({"file": Path(f).name, "taxa_packed": int(p.n_taxa), "kept_gpu": int(len(got)),
+                          "kept_oracle": int(keep.sum()), "same_kept_taxa": same_set, "max_rel": worst,
+                          "worst_field": wf, "within_1e-4": worst < 1e-4, "oracle_s": round(cpu_s, 2),
+                          "oracle_threads": threads}), flush=True)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--files", type=int, default=10)
@@ -137,6 +182,7 @@ def main() -> None:
     ap.add_argument("--readers", type=int, default=0, help="files read ahead (main.N_READERS; 0: its default)")
     ap.add_argument("--arrow-threads", type=int, default=0, help="pyarrow.set_cpu_count (0: Arrow's default)")
     ap.add_argument("--trace", action="store_true", help="print the per-thread stage timeline of the driver run")
+    ap.add_argument("--check", action="store_true", help="then check every file's result frame against the oracle")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -196,6 +242,11 @@ def main() -> None:
         print(json.dumps({"config": "C5", "inference": a.inference, "files": a.files, "ranks": world,
                           "taxa_fitted": taxa, "wall_s": round(wall, 3), "taxa_per_s": round(taxa / wall, 1),
                           "s_per_file": round(wall * world / a.files, 3)}), flush=True)
+    if a.check:
+        from metadamage_amd.utils import extract_name
+
+        mine = [f for f in files if extract_name(f) in res]
+        check(mine, d / "out", a.inference)
     if world > 1:
         dist.destroy_process_group()
 
