@@ -1114,6 +1114,17 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PPL == 1 
 #ifndef MDFIT_NUTS_STEAL
 #define MDFIT_NUTS_STEAL 1  // chain waves take tasks from the other XCDs' queues once theirs runs dry
 #endif
+// a wave whose chain has run long takes issue priority over its SIMD's other
+// waves (s_setprio 1 / 2 / 3 past 32k / 64k / 128k wave-trips since the chain
+// started): the kernel ends with its longest chain (C3: 2-4.5e5 trips, ~15 us
+// a trip at full load, 4.8 s -- as long as the call), so those trips are the
+// critical path; checked every 256 trips
+#ifndef MDFIT_NUTS_PRIO
+#define MDFIT_NUTS_PRIO 1
+#endif
+#ifndef MDFIT_NUTS_PRIO_T
+#define MDFIT_NUTS_PRIO_T 32768.0  // trips of the first level (x2, x4 for the next)
+#endif
 #ifndef MDFIT_NUTS_CD_WAVES
 #define MDFIT_NUTS_CD_WAVES 4  // 128 VGPRs, no spill with MachineLICM off (build_hip)
 #endif
@@ -1328,6 +1339,10 @@ struct ColdState {
   double st_div, st_leap;
   int sub, attempt, f_call, f_m, f_last, f_dir, t_da, widx, wn, nm_chunk;
   int t_n, t_depth;
+  double t_start;  // the wave's trip count when the chain started (MDFIT_NUTS_PRIO)
+#ifdef MDFIT_DEV_TRIPS  // development: per-chain start / end clock and trips in diag 4, 5, 7
+  double dev_t0, dev_c0;
+#endif
 };
 
 template <int PPL>
@@ -1518,6 +1533,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       }
       C.st = make_stream(o.seed, o.index_base + taxon, sub);
       C.nm_chunk = -1;
+#ifndef MDFIT_NO_UTIL
+      C.t_start = (double)util_trips;
+#endif
+#ifdef MDFIT_DEV_TRIPS
+      C.dev_t0 = (double)util_trips;
+      C.dev_c0 = (double)__builtin_amdgcn_s_memrealtime();
+#endif
       mode = kInit;
       C.attempt = 0;
       it = 0;
@@ -1543,6 +1565,15 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       util_trips += 1;
       util_busy += __popcll(rb);
     }
+#if MDFIT_NUTS_PRIO
+    if ((util_trips & 255ull) == 0ull) {
+      const double age = running ? (double)util_trips - C.t_start : 0.0;
+      if (__any(age > 4.0 * MDFIT_NUTS_PRIO_T)) __builtin_amdgcn_s_setprio(3);
+      else if (__any(age > 2.0 * MDFIT_NUTS_PRIO_T)) __builtin_amdgcn_s_setprio(2);
+      else if (__any(age > MDFIT_NUTS_PRIO_T)) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
+#endif
 #endif
     const bool pmd = pmdq;
     const bool act = active(pmd, c);
@@ -1805,7 +1836,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
           if (it == W + S) {
             if ((!whole || h == 0) && i < 4) {
               double* dg = out + C.taxon * MDFIT_NOUT + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * C.sub;
+#ifdef MDFIT_DEV_TRIPS
+              dg[4 + i] = i == 0 ? C.dev_c0 : (i == 1 ? (double)__builtin_amdgcn_s_memrealtime() : (i == 2 ? (double)MDFIT_OK : (double)util_trips - C.dev_t0));
+#else
               dg[4 + i] = i == 0 ? C.eps : (i == 1 ? C.st_leap / S : (i == 2 ? (double)MDFIT_OK : C.st_div));
+#endif
             }
             mode = kDone;
           } else if (!begin_find) {
