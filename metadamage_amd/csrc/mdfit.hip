@@ -44,6 +44,17 @@
 #include "mdfit_model.h"
 #include "mdfit_special.h"
 
+#ifdef MDFIT_DEV_HPTIME
+// development: clock stamps of the MAP call's HPDI hand-off (tools/_hptime.py):
+// [0, T) PMD-all mode published, [T, 2T) the taxon's pair done, then per item
+// taken and written (T * 30 each)
+__device__ unsigned long long* g_dev_hpt = nullptr;
+#define MDFIT_DEV_T(idx) \
+  do {                     \
+    if (g_dev_hpt != nullptr) g_dev_hpt[(idx)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#endif
+
 namespace mdfit {
 
 constexpr int kAll = 0, kFR = 1;
@@ -847,6 +858,9 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
           const bool badB = PPL == 2 && vB_all && pb.y > pb.N;
           const bool bad = (__ballot(badA || badB) & slot_mask) != 0ull;
           if (r == 0) {
+#ifdef MDFIT_DEV_HPTIME
+            MDFIT_DEV_T(taxon);
+#endif
             const int idx = atomicAdd(ws + kWsReady, 1);
             uint64_t* e = reinterpret_cast<uint64_t*>(ready + (int64_t)idx * kReadyStride);
             ready_put(e + 0, bad ? NAN : sig(u[0]));
@@ -858,6 +872,9 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
         }
         mode = kNextPair;
       } else if (mode == kPairFit) {
+#ifdef MDFIT_DEV_HPTIME
+        if (r == 0) MDFIT_DEV_T(T + taxon);
+#endif
         mode = kIdle;
       }
     }
@@ -1367,6 +1384,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
           wide = !hpdi::prep_position(N, D * phi, (1.0 - D) * phi, lo, hi, rec);
           if (wide) hpdi::wide_start(W, rec);
         }
+#ifdef MDFIT_DEV_HPTIME
+        if (sane) MDFIT_DEV_T(2 * T + oitem);
+        if (sane && !wide) MDFIT_DEV_T(2 * T + n_items + oitem);
+#endif
         if (wide) busy = true;
         else if (sane) hpdi_write<true>(io, oitem, N, lo, hi);
         pending = false;
@@ -1386,6 +1407,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
         double lo, hi;
         hpdi::wide_finish(W, lo, hi);
         hpdi_write<true>(io, oitem, W.P.N, lo, hi);
+#ifdef MDFIT_DEV_HPTIME
+        MDFIT_DEV_T(2 * T + n_items + oitem);
+#endif
         busy = false;
       }
     }
@@ -1705,6 +1729,12 @@ int launch_hpdi(const mdfit::HpdiIO& io, int64_t n_items, int* ctr, mdfit::hpdi:
 void mdfit::host::prof_mark(int slot, hipStream_t s) { prof_record(slot, s); }
 
 extern "C" {
+
+#ifdef MDFIT_DEV_HPTIME
+int mdfit_dev_set_hptime(unsigned long long* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_dev_hpt), &buf, sizeof(buf)) != hipSuccess;
+}
+#endif
 
 int mdfit_profile_enable(int on) {
   if (on && !g_prof.made) {
