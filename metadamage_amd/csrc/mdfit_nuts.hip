@@ -1122,6 +1122,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PPL == 1 
 #ifndef MDFIT_NUTS_PRIO
 #define MDFIT_NUTS_PRIO 1
 #endif
+#ifndef MDFIT_NUTS_COLD_LEAF
+#define MDFIT_NUTS_COLD_LEAF 1
+#endif
 #ifndef MDFIT_NUTS_PRIO_T
 #define MDFIT_NUTS_PRIO_T 32768.0  // trips of the first level (x2, x4 for the next)
 #endif
@@ -1327,7 +1330,7 @@ __device__ __forceinline__ bool turning_full(bool pmd, const double invm[4], con
 }
 
 // per-slot LDS vectors (component c at [c])
-enum { kVlz, kVlr, kVlg, kVrz, kVrr, kVrg, kVtz, kVtg, kVsz, kVsg, kVwm, kVw2, kVim, kVis, kVtr, kNVec };
+enum { kVlz, kVlr, kVlg, kVrz, kVrr, kVrg, kVtz, kVtg, kVsz, kVsg, kVwm, kVw2, kVim, kVis, kVtr, kVss, kNVec };
 
 // cold per-chain scalars (row-uniform, LDS)
 struct ColdState {
@@ -1340,6 +1343,8 @@ struct ColdState {
   int sub, attempt, f_call, f_m, f_last, f_dir, t_da, widx, wn, nm_chunk;
   int t_n, t_depth;
   double t_start;  // the wave's trip count when the chain started (MDFIT_NUTS_PRIO)
+  double s_acc;    // (MDFIT_NUTS_COLD_LEAF) the subtree's acceptance sum,
+  int s_n, ul_chunk;  // size and the chunk of leaf uniforms in sul
 #ifdef MDFIT_DEV_TRIPS  // development: per-chain start / end clock and trips in diag 4, 5, 7
   double dev_t0, dev_c0;
 #endif
@@ -1427,12 +1432,29 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
 
   // hot chain state, row-uniform (the vectors: component c)
   int mode = 0, drained = 0, whole = 0, it = 0;
-  double z = 0.0, rm = 0.0, gr = 0.0, im = 1.0, srs = 0.0;
+  double z = 0.0, rm = 0.0, gr = 0.0, im = 1.0;
+  // (the subtree's momentum sum: V[kVss], component c -- a register it was spilled)
   // (the tree's scalars -- weight, acceptance sum, size, depth, merge uniform --
   // and the step size are touched once per doubling: ColdState)
   double step = 0.0, e0 = 0.0;
+#if MDFIT_NUTS_COLD_LEAF
+  // (the subtree's acceptance sum and size and the leaf-uniform chunk live in
+  // the row's ColdState: touched once a leaf, they were the kernel's spills)
+  double s_w = 0.0;
+  int leaf_ctr = 0, nleap = 0, n_leaf = 0, nmax = 1;
+  C.s_acc = 0.0;
+  C.s_n = 0;
+  C.ul_chunk = -1;
+#define MDFIT_CD_SACC C.s_acc
+#define MDFIT_CD_SN C.s_n
+#define MDFIT_CD_ULC C.ul_chunk
+#else
   double s_w = 0.0, s_acc = 0.0;
   int leaf_ctr = 0, nleap = 0, s_n = 0, n_leaf = 0, nmax = 1, ul_chunk = -1;
+#define MDFIT_CD_SACC s_acc
+#define MDFIT_CD_SN s_n
+#define MDFIT_CD_ULC ul_chunk
+#endif
   int right = 1, t_turn = 0, t_div = 0, s_div = 0;
 // slot utilisation and the point-evaluation count (bench.py's compute
 // roofline): wave-trips with a running slot, and running slot-trips (each one
@@ -1673,22 +1695,22 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         V[kVsz][c] = zev;
         V[kVsg][c] = P.g;
         C.spe = P.U;
-        srs = rn;
+        V[kVss][c] = rn;
         s_w = w;
-        s_acc = acc;
-        s_n = 1;
+        MDFIT_CD_SACC = acc;
+        MDFIT_CD_SN = 1;
       } else {
         const double m = fmax(s_w, w);
         const double e = exp(-fabs(s_w - w));
         const double nw = m == -INFINITY ? -INFINITY : m + lae1p(e);
         const double prob = (w >= s_w ? 1.0 : e) * rcp(1.0 + e);
-        if ((leaf_ctr >> 4) != ul_chunk) {  // next 16 leaf uniforms, 16 / kG per lane
+        if ((leaf_ctr >> 4) != MDFIT_CD_ULC) {  // next 16 leaf uniforms, 16 / kG per lane
 #pragma unroll
           for (int e2 = 0; e2 < 16 / kG; ++e2) {
             const int ix = i + kG * e2;
             sul[row16 + ix] = uniform(C.st, (uint32_t)it, 32u + (uint32_t)(leaf_ctr & ~15) + (uint32_t)ix);
           }
-          ul_chunk = leaf_ctr >> 4;
+          MDFIT_CD_ULC = leaf_ctr >> 4;
         }
         if (sul[row16 + (leaf_ctr & 15)] < prob) {
           V[kVsz][c] = zev;
@@ -1696,15 +1718,16 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
           C.spe = P.U;
         }
         s_w = nw;
-        srs += rn;
-        s_acc += acc;
-        s_n += 1;
+        V[kVss][c] += rn;
+        MDFIT_CD_SACC += acc;
+        MDFIT_CD_SN += 1;
       }
       s_div = dv;
       ++leaf_ctr;
       NSTAMP(5);
       int imin, imax;
       ckpt_idxs(n_leaf, &imin, &imax);
+      const double srs = V[kVss][c];
       double srs4[4];
       slot4<kG>(srs, srs4);
       if ((n_leaf & 1) == 0 && i == imax) {
@@ -1771,12 +1794,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
           const double m = fmax(C.t_w, s_w);
           C.t_w = m == -INFINITY ? -INFINITY : m + lae1p(em);
         }
-        const double trs = V[kVtr][c] + srs;
+        const double trs = V[kVtr][c] + V[kVss][c];
         V[kVtr][c] = trs;
         t_turn = s_turn || (right ? turning_cd<kG>(act, im, olr, rm, trs) : turning_cd<kG>(act, im, rm, olr, trs));
         t_div = s_div;
-        C.t_acc += s_acc;
-        C.t_n += s_n;
+        C.t_acc += MDFIT_CD_SACC;
+        C.t_n += MDFIT_CD_SN;
         ++C.t_depth;
         if (C.t_depth >= kMaxDepth || t_turn || t_div) {
           NSTAMP(7);
@@ -1923,7 +1946,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         if (ix < 8) sdb[row16 + j] = (int)(b.x & 1u);
         else sut[row16 + j] = u53(b.x, b.y);
       }
-      ul_chunk = -1;
+      MDFIT_CD_ULC = -1;
       right = sdb[row16] != 0;
       C.u_tr = sut[row16];
       n_leaf = 0;
@@ -1932,6 +1955,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
     }
     NSTAMP(4);
   }
+#undef MDFIT_CD_SACC
+#undef MDFIT_CD_SN
+#undef MDFIT_CD_ULC
 #ifdef MDFIT_STAMP
   if (lane == 0 && g_nuts_stamp) {
     unsigned long long* w = g_nuts_stamp + 16 * (size_t)blockIdx.x;
