@@ -2182,9 +2182,7 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
                                                           double* __restrict__ out, float* __restrict__ pred,
                                                           int32_t* __restrict__ status) {
   __shared__ double s_y[kLD], s_N[kLD];
-  __shared__ uint32_t s_mm[kNPos * kNMM];
   __shared__ double s_rec[MDFIT_NOUT];
-  __shared__ double s_tmp[kWave];
   __shared__ double s_waic[MDFIT_NSUBFIT][kNPos];
   // the per-draw values (pointwise log-likelihoods, predictive fractions): the
   // launch sizes it to the sort's power of two >= S (8 KB at S = 1000; a
@@ -2200,8 +2198,6 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
     s_y[lane] = (double)gy[t * kLD + lane];
     s_N[lane] = (double)gN[t * kLD + lane];
   }
-  if (gmm != nullptr)
-    for (int x = lane; x < kNPos * kNMM; x += kWave) s_mm[x] = gmm[t * (kNPos * kNMM) + x];
   for (int x = lane; x < MDFIT_NOUT; x += kWave)
     s_rec[x] = (x >= MDFIT_NRESULT && x < MDFIT_F_DIAG) ? 0.0 : out[t * MDFIT_NOUT + x];
   __syncthreads();
@@ -2408,6 +2404,13 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
     }
   }
   __syncthreads();
+  // the mismatch counts and the noise scratch reuse the draws' LDS (the kernel
+  // is LDS-limited: 8.6 -> 6.7 KB per wave; the launch sizes it >= 2 KB)
+  uint32_t* s_mm = s_c;
+  double* s_tmp = reinterpret_cast<double*>(s_c + kNPos * kNMM);
+  if (gmm != nullptr)
+    for (int x = lane; x < kNPos * kNMM; x += kWave) s_mm[x] = gmm[t * (kNPos * kNMM) + x];
+  __syncthreads();
   record_sums_noise(lane, s_y, s_N, s_mm, gmm != nullptr, s_rec, s_tmp);
   __syncthreads();
   for (int x = lane; x < MDFIT_NOUT; x += kWave) out[t * MDFIT_NOUT + x] = s_rec[x];
@@ -2555,6 +2558,8 @@ int fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t 
   const size_t elt = MDFIT_POST_U32 ? sizeof(uint32_t) : sizeof(double);
   size_t sv_bytes = elt;
   while (sv_bytes < (size_t)o.num_samples * elt) sv_bytes <<= 1;  // the sort pads to 2^k
+  // (the noise's counts and scratch reuse it after the draws: 1440 + 512 B)
+  sv_bytes = sv_bytes < 2048 ? 2048 : sv_bytes;
   host::debug_poison(s);
   hipLaunchKernelGGL(nuts_post_kernel, dim3((unsigned)n_taxa), dim3(kWave), sv_bytes, s, y, N, mm, n_taxa, o,
                      samples, out, pred, status);
