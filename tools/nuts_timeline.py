@@ -22,7 +22,6 @@ res = engine.alloc_outputs(T, opts=o)
 res.workspace = torch.empty(int(lib.mdfit_workspace_bytes(T, ctypes.byref(o))), dtype=torch.uint8, device="cuda")
 dump = {}
 for order in (0,):
-    os.environ["MDFIT_NUTS_ORDER"] = str(order)
     _lib.check(lib.mdfit_fit_batch(ctypes.c_void_p(ty.data_ptr()), ctypes.c_void_p(tN.data_ptr()), ctypes.c_void_p(tm.data_ptr()), T, ctypes.byref(o), ctypes.c_void_p(res.out.data_ptr()), ctypes.c_void_p(res.pred.data_ptr()), ctypes.c_void_p(res.status.data_ptr()), ctypes.c_void_p(res.workspace.data_ptr()), None))
     torch.cuda.synchronize()
     out = res.out.cpu().numpy()
