@@ -131,6 +131,22 @@ def test_sampling_is_deterministic_and_keyed_by_index_base(nuts_engine):
     np.testing.assert_array_equal(a[0][3:], p[0])
 
 
+def test_records_do_not_depend_on_which_wave_runs_a_chain(nuts_engine, monkeypatch):
+    """The chain kernel's scheduling -- per-XCD queues, stealing across them,
+    the long-chain issue priority -- decides only which wave runs a chain and
+    when: the streams are keyed by (taxon, sub-fit), so a grid of 1 wave per CU
+    (every wave runs many chains, the queues drain in another order) gives the
+    default grid's records bit for bit."""
+    from metadamage_amd.synthetic import generate
+
+    b = generate(600, seed=9)
+    a = _run(nuts_engine, b, 40, 60)
+    monkeypatch.setenv("MDFIT_DEV_PER_CU", "1")
+    c = _run(nuts_engine, b, 40, 60)
+    for x, y in zip(a, c):
+        np.testing.assert_array_equal(x.view(np.uint8), y.view(np.uint8))
+
+
 def test_invalid_and_empty_positions(nuts_engine):
     from metadamage_amd.synthetic import generate
 
