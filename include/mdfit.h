@@ -100,7 +100,11 @@ enum mdfit_field {
    * objective, evaluations, status, polished}.  Null sub-fits store A = c = 0.
    * MAP: `polished` = 1 when the fit entered its polish phase (DESIGN.md
    * §3.4); its objective is then the cancellation-free form (the full log-pmf,
-   * log C(N,y) included), else the lnGamma-sum form.  NUTS: {posterior means
+   * log C(N,y) included), else the lnGamma-sum form.  After the MDFIT-MAP
+ * v1.1 quadratic-contraction stop the returned point is u + d
+ * (the last Newton step taken without evaluating its end) while `objective`
+ * holds F at the last EVALUATED point u: it exceeds F(u + d) by O(|g.d|) <=
+ * ~1e-9 relative (the oracle stores the same).  NUTS: {posterior means
    * of q, A, c, phi, adapted step size, leapfrogs per draw, status,
    * divergences}. */
   MDFIT_F_DIAG = 32,
@@ -138,13 +142,18 @@ void mdfit_default_opts(mdfit_opts* opts);
  *   workspace : device buffer of mdfit_workspace_bytes(n_taxa) bytes (work
  *               queues, the PMD-all mode for the HPDI, the wide-window list:
  *               MAP 256 B + 48 B per taxon below 60k taxa, + 4,800 B more
- *               per taxon from 60k, + the HPDI stream's defer list:
- *               min(120 B per taxon, 512 KB))
- *   hip_stream: hipStream_t or NULL.  MAP: the record assembly runs on a
- *               library-owned side stream (one per device, created once),
+ *               per taxon from 60k (160 B per position's wide-window record),
+ *               + the HPDI stream's defer list: min(120 B per taxon, 512 KB);
+ *               NUTS 256 B + 6 x num_samples x 32 B per taxon, the draws)
+ *   hip_stream: hipStream_t or NULL.  MAP: parts of the call run on two
+ *               library-owned side streams (one set per device, created once),
  *               forked from and joined back into hip_stream by events on every
  *               return path, so the call stays ordered on hip_stream and
- *               capturable in a graph.  MAP below 60k taxa: the predictive
+ *               capturable in a graph: below 60k taxa the early HPDI launch
+ *               beside the fit kernel and the late HPDI launch beside the
+ *               record assembly (which follows the fit on hip_stream); from
+ *               60k taxa the record assembly beside the HPDI launches (which
+ *               stay on hip_stream).  MAP below 60k taxa: the predictive
  *               HPDI kernel runs beside the fit kernel and waits for modes
  *               the fit kernel's waves publish (relaxed, order-free: each
  *               field of a ready-list entry is written once as the bit

@@ -22,6 +22,9 @@
 #include <cstring>
 #include <string>
 #include <string_view>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -275,6 +278,54 @@ void parallel_chunks(std::vector<Chunk>& chunks, F f) {
 
 }  // namespace
 
+// The release worker of mdi_free: one thread, started on the first deferred
+// release, fed through a queue, drained and joined when the library unloads
+// (static destructor: exit(), or dlclose of the last handle).
+static void release_table(mdi_table* x) {
+  if (x->map && x->map != MAP_FAILED) munmap(x->map, x->size);
+  delete x;
+}
+
+namespace {
+struct ReleaseWorker {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<mdi_table*> q;
+  std::thread th;
+  bool stop = false;
+
+  void push(mdi_table* t) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      q.push_back(t);
+      if (!th.joinable()) th = std::thread([this] { run(); });
+    }
+    cv.notify_one();
+  }
+  void run() {
+    std::unique_lock<std::mutex> g(mu);
+    while (true) {
+      cv.wait(g, [this] { return stop || !q.empty(); });
+      if (q.empty()) return;  // (stop, and nothing left)
+      mdi_table* t = q.front();
+      q.pop_front();
+      g.unlock();
+      release_table(t);
+      g.lock();
+    }
+  }
+  ~ReleaseWorker() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      stop = true;
+    }
+    cv.notify_one();
+    if (th.joinable()) th.join();
+  }
+};
+ReleaseWorker g_release;
+}  // namespace
+
 extern "C" {
 
 int mdi_default_threads(void) {
@@ -448,14 +499,13 @@ void mdi_free(mdi_table* t) {
   if (!t) return;
   // unmapping a populated 300 MB mapping takes ~20 ms of page-table teardown,
   // and the chunks' string tables (~1e5 hash nodes and strings per file) ~8 ms
-  // of frees: both on a detached thread (nothing views the mapping or the
-  // tables any more: the caller copied the strings out with mdi_strings)
-  auto release = [](mdi_table* x) {
-    if (x->map && x->map != MAP_FAILED) munmap(x->map, x->size);
-    delete x;
-  };
-  if (t->size >= ((size_t)1 << 24)) std::thread(release, t).detach();
-  else release(t);
+  // of frees: both off the caller's thread (nothing views the mapping or the
+  // tables any more: the caller copied the strings out with mdi_strings), on
+  // the library's release worker, which the library's destructor drains and
+  // joins -- a process that exits right after its last mdi_free does not race
+  // the allocator's teardown
+  if (t->size >= ((size_t)1 << 24)) g_release.push(t);
+  else release_table(t);
 }
 
 const char* mdi_last_error(void) { return g_err; }

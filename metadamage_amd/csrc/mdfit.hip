@@ -318,10 +318,6 @@ __device__ __forceinline__ void hpdi_position(const HpdiIO& io, int64_t item, bo
   }
 }
 
-#ifndef MDFIT_LDS_SUMS
-#define MDFIT_LDS_SUMS 1  // fit_kernel's sums through LDS (0: the register butterfly; bitwise-identical)
-#endif
-
 // the butterfly's summation tree over 8 / 16 values in lane order: pairs
 // (xor 1), pairs of pairs (xor 2), the two quads (half mirror), the two halves
 // (mirror) -- sets, so the order inside each add does not matter
@@ -384,13 +380,11 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
   pb.k = kB_all;
   pa.pmd = pb.pmd = true;
 
-#if MDFIT_LDS_SUMS
   // the sums' LDS: the lanes' terms accumulator-major (row stride padded by 2
   // doubles: a row's 16 lanes then read 16 consecutive 16-B slots, no bank
   // conflict) and the finished sums (PPL 2: one set per half)
   __shared__ __attribute__((aligned(16))) double sAcc[kNAcc][kWave + 2];
   __shared__ __attribute__((aligned(16))) double sSum[2][kWave];
-#endif
   // the HPDI stream kernel running beside this one waits only once it has
   // seen this flag (no wait on a kernel that may not be running)
   if (blockIdx.x == 0 && lane == 0)
@@ -536,32 +530,32 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
       const bool src15 = whole || h == 1;
       auto pad3 = [&](const LG3& v) -> LG3 { return src15 ? rowb3<15>(v) : rowb3<7>(v); };
       const PointArgs gb = point_args(pb, th);
-      const LG3 t3b = lg3<true, MDFIT_TLOG_FIT>(pb.N + th.phi);
+      const LG3 t3b = lg3<true>(pb.N + th.phi);
       const LG3 t6 = pad3(t3b);
-      const LG3 tb1 = lg3<true, MDFIT_TLOG_FIT>(pb.y + gb.a);
-      const LG3 tb2 = lg3<true, MDFIT_TLOG_FIT>(pb.N - pb.y + gb.b);
+      const LG3 tb1 = lg3<true>(pb.y + gb.a);
+      const LG3 tb2 = lg3<true>(pb.N - pb.y + gb.b);
       LG3 tb4, tb5;
       if (null_wave) {
         tb4 = pad3(tb1);
         tb5 = pad3(tb2);
       } else {
-        tb4 = lg3<true, MDFIT_TLOG_FIT>(gb.a);
-        tb5 = lg3<true, MDFIT_TLOG_FIT>(gb.b);
+        tb4 = lg3<true>(gb.a);
+        tb5 = lg3<true>(gb.b);
       }
       double accb[kNAcc];
 #pragma unroll
       for (int j = 0; j < kNAcc; ++j) accb[j] = 0.0;
       point_finish(pb, th, gb, tb1, tb2, t3b, tb4, tb5, t6, accb, accf);
       const PointArgs ga = point_args(pa, th);
-      const LG3 ta3 = lg3<true, MDFIT_TLOG_FIT>(pa.N + th.phi);
-      const LG3 ta1 = lg3<true, MDFIT_TLOG_FIT>(pa.y + ga.a);
-      const LG3 ta2 = lg3<true, MDFIT_TLOG_FIT>(pa.N - pa.y + ga.b);
+      const LG3 ta3 = lg3<true>(pa.N + th.phi);
+      const LG3 ta1 = lg3<true>(pa.y + ga.a);
+      const LG3 ta2 = lg3<true>(pa.N - pa.y + ga.b);
       // (null: a, b are the half's; an all-position fit: point a is z = +k,
       // point b z = -k, the same a, b; a pair: the point's own)
       LG3 ta4 = tb4, ta5 = tb5;
       if (!null_wave && !whole_wave) {
-        ta4 = lg3<true, MDFIT_TLOG_FIT>(ga.a);
-        ta5 = lg3<true, MDFIT_TLOG_FIT>(ga.b);
+        ta4 = lg3<true>(ga.a);
+        ta5 = lg3<true>(ga.b);
       }
       point_finish(pa, th, ga, ta1, ta2, ta3, ta4, ta5, t6, acc, accf);
 #pragma unroll
@@ -571,13 +565,11 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
     const unsigned long long e1 = stamp();
 #endif
     // sums over the slot's positions (all-position fits) or the half's
-#if MDFIT_LDS_SUMS
     // Through LDS, accumulator-major: every lane writes its 16 terms to
     // sAcc[j][lane], then lane i of a row forms the row's sum of accumulator i
-    // (tree16 / tree8: the butterfly's summation tree, so the same bits as the
-    // register butterfly below and in both layouts), and the sums come back to
-    // every lane of the row from sSum.  ~60 VALU per trip instead of ~240 DPP
-    // moves and adds.
+    // (tree16 / tree8: a register butterfly's summation tree, so the same bits
+    // in both layouts), and the sums come back to every lane of the row from
+    // sSum.  ~60 VALU per trip instead of ~240 DPP moves and adds (round 5).
 #pragma unroll
     for (int j = 0; j < kNAcc; ++j) sAcc[j][lane] = acc[j];
     __syncthreads();
@@ -614,29 +606,6 @@ void fit_kernel(const uint32_t* __restrict__ gy, const uint32_t* __restrict__ gN
 #pragma unroll
       for (int j = 0; j < kNAcc; ++j) acc[j] = src[j];
     }
-#else
-    // PPL 1: every accumulator's cross-row partner (xor 16, ds_bpermute) is
-    // requested before the first one is used, so the 16 LDS round trips
-    // overlap (one accumulator at a time, each waited for by its own
-    // lgkmcnt(0), cost ~1.5k cycles per trip)
-    if (PPL == 1) {
-      double o[kNAcc];
-#pragma unroll
-      for (int j = 0; j < kNAcc; ++j) acc[j] = opaque(acc[j]);
-#pragma unroll
-      for (int j = 0; j < kNAcc; ++j) o[j] = __shfl_xor(acc[j], 16, 64);
-#pragma unroll
-      for (int j = 0; j < kNAcc; ++j) acc[j] = gsum<16>(whole ? acc[j] + o[j] : acc[j]);
-    }
-    if (PPL == 2) {
-#pragma unroll
-      for (int j = 0; j < kNAcc; ++j) {
-        const double s8 = gsum<8>(acc[j]);
-        const double s16 = s8 + dpp<0x140>(s8);  // row_mirror: the other half's sum
-        acc[j] = whole ? s16 : s8;
-      }
-    }
-#endif
 #ifdef MDFIT_STAMP
     const unsigned long long e2 = stamp();
 #endif
@@ -1448,7 +1417,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_HPD
 __global__ void special_kernel(const double* __restrict__ x, int64_t n, double* __restrict__ o) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const LG3 r = lg3<true, MDFIT_TLOG_FIT>(x[i]);  // (the fit kernel's form, the one its parity test covers)
+  const LG3 r = lg3<true>(x[i]);  // (the fit kernel's form, the one its parity test covers)
   o[3 * i + 0] = r.l;
   o[3 * i + 1] = r.p;
   o[3 * i + 2] = r.q;
@@ -1644,8 +1613,10 @@ mdfit::hpdi::WideRec* hpdi_recs_after_ready(void* ws, int64_t n_taxa) {
                                                  n_taxa * mdfit::kReadyStride * (int64_t)sizeof(double));
 }
 
-// The side streams of mdfit_fit_batch's forks -- [0] the HPDI stream kernel
-// beside the fit kernel, [1] the record assembly beside the late HPDI launch --
+// The side streams of mdfit_fit_batch's forks -- [0] the early HPDI stream
+// launch beside the fit kernel, [1] the second fork after the fit (below 60k
+// taxa the late HPDI launch beside the record assembly, from 60k the record
+// assembly beside K4a -> K4b) --
 // and their fork / join events: one set per device, created on first use and
 // kept for the process (bounded: 2 streams per device, not per calling host
 // thread); the streams non-blocking (ordered against the caller's stream by the
@@ -1890,18 +1861,17 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   }
   if (int rc = check_launch("fit_kernel")) return rc;
   prof_record(2, s);
-  // then a fork: the record assembly (K3) on side stream 1, the HPDI's late
-  // launch on the caller's stream (full occupancy, draining what the early
-  // one left); they write disjoint fields of the record and join before the
-  // call returns
+  // then a fork onto side stream 1: the record assembly (K3) and the HPDI's
+  // late launch / K4a -> K4b run side by side; they write disjoint fields of
+  // the record and join before the call returns
   ForkScope fork_as(fk, s, 1);
   // Below kStreamMaxTaxa the record assembly follows the fit on the caller's
   // stream (it starts as soon as the fit ends; on the side stream it waited
   // ~30 us longer for the fork event) and the HPDI's late launch -- a short
-  // drain of what the early launch left -- takes the side stream;
-  // MDFIT_ASM_SIDE=1 restores the old placement (A/B).  From kStreamMaxTaxa
-  // the HPDI (K4a -> K4b) is the long part and keeps the caller's stream.
-  const bool asm_main = stream && env_int("MDFIT_ASM_SIDE", 0) == 0;
+  // drain of what the early launch left -- takes the side stream.  From
+  // kStreamMaxTaxa the HPDI (K4a -> K4b) is the long part and keeps the
+  // caller's stream.
+  const bool asm_main = stream;
   const hipStream_t s_asm = asm_main ? s : fork_as.side();
   const hipStream_t s_hp = asm_main ? fork_as.side() : s;
   mdfit::host::debug_poison(s_asm);

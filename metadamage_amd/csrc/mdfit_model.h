@@ -298,23 +298,23 @@ template <bool kRowPhi = false>
 __device__ __forceinline__ double point_accum(const PointData& pd, const Theta& th, double acc[kNAcc],
                                               int accf = 0, bool null_row = false, bool whole_pair = false) {
   const PointArgs pa = point_args(pd, th);
-  const LG3 t3 = lg3<true, MDFIT_TLOG_FIT>(pd.N + th.phi);
-  const LG3 t6 = kRowPhi ? rowb3<15>(t3) : lg3<true, MDFIT_TLOG_FIT>(th.phi);
-  const LG3 t1 = lg3<true, MDFIT_TLOG_FIT>(pd.y + pa.a);
-  const LG3 t2 = lg3<true, MDFIT_TLOG_FIT>(pd.N - pd.y + pa.b);
+  const LG3 t3 = lg3<true>(pd.N + th.phi);
+  const LG3 t6 = kRowPhi ? rowb3<15>(t3) : lg3<true>(th.phi);
+  const LG3 t1 = lg3<true>(pd.y + pa.a);
+  const LG3 t2 = lg3<true>(pd.N - pd.y + pa.b);
   LG3 t4, t5;
   if (kRowPhi && null_row) {
     t4 = rowb3<15>(t1);
     t5 = rowb3<15>(t2);
   } else if (kRowPhi && whole_pair) {
     const bool odd = (threadIdx.x & 16) != 0;
-    const LG3 mine = lg3<true, MDFIT_TLOG_FIT>(odd ? pa.b : pa.a);
+    const LG3 mine = lg3<true>(odd ? pa.b : pa.a);
     const LG3 other = {xrow(mine.l), xrow(mine.p), xrow(mine.q)};
     t4 = odd ? other : mine;
     t5 = odd ? mine : other;
   } else {
-    t4 = lg3<true, MDFIT_TLOG_FIT>(pa.a);
-    t5 = lg3<true, MDFIT_TLOG_FIT>(pa.b);
+    t4 = lg3<true>(pa.a);
+    t5 = lg3<true>(pa.b);
   }
   return point_finish(pd, th, pa, t1, t2, t3, t4, t5, t6, acc, accf);
 }

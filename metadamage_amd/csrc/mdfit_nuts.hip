@@ -4,17 +4,16 @@
 // num_warmup 500 / num_samples 1000, one chain) and post-processes the draws
 // (fits.py:89-172, 230-356).  Two launches:
 //
-//   nuts_chain_kernel  persistent, the MAP kernel's lane layout: a wave = 2
-//                      groups of 32 lanes, a group = 2 rows of 16, lane =
-//                      position (lane 15 of a row a pad).  A group runs one
-//                      all-position chain (rows' sums added, identical state)
-//                      or the forward/reverse pair of one model (a chain per
-//                      row).  Every trip every running chain does ONE
-//                      potential + gradient evaluation -- a leapfrog step, an
-//                      initial-point probe or a step-size-search step -- and
-//                      then advances its state machine (iterative NUTS tree,
-//                      Stan-window adaptation).  Kept draws go to the
-//                      workspace: double[T][6][S][4] = (q, A, c, phi).
+//   nuts_chain_cd      persistent, component-distributed: a 16-lane slot is
+//                      one chain (an all-position chain two slots), lane =
+//                      position (lane 15 of a row a pad), and lane i also
+//                      holds component i & 3 of the chain's 4-vectors.  Every
+//                      trip every running chain does ONE potential + gradient
+//                      evaluation -- a leapfrog step, an initial-point probe
+//                      or a step-size-search step -- and then advances its
+//                      state machine (iterative NUTS tree, Stan-window
+//                      adaptation).  Kept draws go to the workspace:
+//                      double[T][6][S][4] = (q, A, c, phi).
 //   nuts_post_kernel   one wave per taxon, lanes over draws: pointwise
 //                      log-likelihood -> lppd / pWAIC / waic_i, n_sigma x3,
 //                      asymmetry, posterior means, predictive Beta-Binomial
@@ -114,12 +113,7 @@ __device__ __forceinline__ double uniform(const Stream& s, uint32_t w2, uint32_t
 // not inlined: its log / cos / sqrt temporaries then stay out of the chain
 // loop's register allocation (fewer spills on the hot path; measured -4 % C3
 // together with the momentum cache)
-#ifndef MDFIT_NORMAL_INLINE
-__device__ __noinline__
-#else
-__device__ __forceinline__
-#endif
-double normal(const Stream& s, uint32_t w2, uint32_t w3) {
+__device__ __noinline__ double normal(const Stream& s, uint32_t w2, uint32_t w3) {
   const uint4 o = block(s, w2, w3);
   const double u1 = 1.0 - u53(o.x, o.y), u2 = u53(o.z, o.w);
   return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
@@ -129,10 +123,6 @@ __device__ __forceinline__ double normal_inl(const Stream& s, uint32_t w2, uint3
   const uint4 o = block(s, w2, w3);
   const double u1 = 1.0 - u53(o.x, o.y), u2 = u53(o.z, o.w);
   return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
-}
-
-__device__ __forceinline__ double sel4(const double v[4], int j) {
-  return j == 0 ? v[0] : (j == 1 ? v[1] : (j == 2 ? v[2] : v[3]));
 }
 
 __device__ __forceinline__ bool active(bool pmd, int j) { return pmd || j == 0 || j == 3; }
@@ -154,185 +144,6 @@ __device__ __forceinline__ void slot4(double v, double out[4]) {
     out[2] = hi8 ? rowb<10>(v) : rowb<2>(v);
     out[3] = hi8 ? rowb<11>(v) : rowb<3>(v);
   }
-}
-
-// ---------------------------------------------------------------------------
-// potential (oracle: nuts_potential), row-collective
-// ---------------------------------------------------------------------------
-struct Pot {
-  double U;
-  double g[4];
-};
-
-// -(log density + log|J|) of the row's (or, `whole`, the group's) points at
-// v and its gradient.  Lanes 0-2 of a row resolve sigmoid(v0..v2), lane 3
-// exp(v3); the phi triple is the pad lane's lg(0 + phi).
-__device__ __forceinline__ Pot potential(const PointData& pd, const double v[4], bool whole) {
-  const int i = (int)(threadIdx.x & 15);
-  const double x = i < 3 ? sel4(v, i) : v[3];
-  const double e = exp(i < 3 ? -fabs(x) : x);
-  const double sp = flog1p(e);
-  const double rr = rcp(1.0 + e);
-  const bool pos = x >= 0.0;
-  const double p = pos ? rr : e * rr, omp = pos ? e * rr : rr;
-  const double lp = pos ? -sp : x - sp, l1p = pos ? -(x + sp) : -sp;
-  // prior + log|J|: q, A ~ Beta(2,3) -> 2 ln p + 3 ln(1-p); c ~ Beta(1,9) -> ln c + 9 ln(1-c)
-  const double pr = i == 2 ? lp + 9.0 * l1p : 2.0 * lp + 3.0 * l1p;
-  const double q = rowb<0>(p), omq = rowb<0>(omp), prq = rowb<0>(pr);
-  const double A0 = rowb<1>(p), omA = rowb<1>(omp), prA = rowb<1>(pr);
-  const double c0 = rowb<2>(p), omc = rowb<2>(omp), prc = rowb<2>(pr);
-  const double delta = rowb<3>(e);
-  const double phi = delta + 2.0;
-  const bool pmd = pd.pmd;
-  const double A = pmd ? A0 : 0.0, c = pmd ? c0 : 0.0;
-  // Exponential(rate 1/1000).log_prob = log(rate) - rate * delta (numpyro's form)
-  double lprior = prq + v[3] - delta * 1e-3;
-  if (pmd) lprior += prA + prc;
-
-  double D, dq, dA;
-  if (pmd) {
-    const double w = powk(omq, pd.k);
-    D = fma(A, w, c);
-    dq = pd.k > 0 ? -A * (double)pd.k * (w * rcp(omq)) : 0.0;
-    dA = w;
-  } else {
-    D = q;
-    dq = 1.0;
-    dA = 0.0;
-  }
-  const bool bad_lane = (pd.valid && !(D < 1.0)) || (pmd && A + c >= 1.0);
-  const double a = D * phi, b = (1.0 - D) * phi;
-  const LG3 t1 = lg3<false, MDFIT_TLOG_NUTS>(pd.y + a);
-  const LG3 t4 = lg3<false, MDFIT_TLOG_NUTS>(a);
-  const double la = t1.l - t4.l, Pa = t1.p - t4.p;
-  const LG3 t2 = lg3<false, MDFIT_TLOG_NUTS>(pd.N - pd.y + b);
-  const LG3 t5 = lg3<false, MDFIT_TLOG_NUTS>(b);
-  const double lb = t2.l - t5.l, Pb = t2.p - t5.p;
-  const LG3 t3 = lg3<false, MDFIT_TLOG_NUTS>(pd.N + phi);
-  const double t6l = rowb<15>(t3.l), t6p = rowb<15>(t3.p);  // pad lane: lg(0 + phi)
-  const double ell = (la + lb) - (t3.l - t6l);
-  const double lD = phi * (Pa - Pb);
-  const double lF = D * Pa + (1.0 - D) * Pb + (t6p - t3.p);
-  double acc[5] = {ell, lD * dq, lD * dA, lD, lF};
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    const double s16 = gsum<16>(pd.valid ? acc[j] : 0.0);
-    acc[j] = whole ? s16 + __shfl_xor(s16, 16, 64) : s16;
-  }
-  const unsigned long long bm = __ballot(bad_lane);
-  const int sh = (int)(threadIdx.x & (whole ? ~31 : ~15));
-  const bool bad = ((bm >> sh) & (whole ? 0xFFFFFFFFull : 0xFFFFull)) != 0ull;
-  Pot o;
-  o.U = -(acc[0] + lprior);
-  o.g[0] = -(acc[1] * (q * omq) + (2.0 - 5.0 * q));
-  o.g[1] = pmd ? -(acc[2] * (A * omA) + (2.0 - 5.0 * A)) : 0.0;
-  o.g[2] = pmd ? -(acc[3] * (c * omc) + (1.0 - 10.0 * c)) : 0.0;
-  o.g[3] = -(acc[4] * delta + (1.0 - delta * 1e-3));
-  if (bad || !isfinite(o.U)) {
-    o.U = INFINITY;
-    o.g[0] = o.g[1] = o.g[2] = o.g[3] = 0.0;
-  }
-  return o;
-}
-
-// The same potential in the two-points-per-lane layout (the chain kernel's
-// PPL 2): a pair chain on 8 lanes (lane j: |z|-1 = 2j, 2j+1 of its direction;
-// lane 7's second point the pad), an all-position chain on 16 (lane j: z = +(j+1)
-// and -(j+1); lane 15 the pad).  Lanes 0-3 of each 8-lane half resolve the
-// sigmoids / exp (an all-position chain's halves hold the same v, so both
-// compute the same values); sums over the half, then across halves (whole).
-__device__ __forceinline__ Pot potential2(const PointData pt[2], const double v[4], bool whole) {
-  const int i = (int)(threadIdx.x & 7);
-  const bool hi8 = threadIdx.x & 8;
-  const double x = i < 3 ? sel4(v, i) : v[3];
-  const double e = exp(i < 3 ? -fabs(x) : x);
-  const double sp = flog1p(e);
-  const double rr = rcp(1.0 + e);
-  const bool pos = x >= 0.0;
-  const double p = pos ? rr : e * rr, omp = pos ? e * rr : rr;
-  const double lp = pos ? -sp : x - sp, l1p = pos ? -(x + sp) : -sp;
-  const double pr = i == 2 ? lp + 9.0 * l1p : 2.0 * lp + 3.0 * l1p;
-  auto bc = [=](double y, auto n) {
-    constexpr int N = decltype(n)::value;
-    return hi8 ? rowb<8 + N>(y) : rowb<N>(y);
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  const double q = bc(p, I0{}), omq = bc(omp, I0{}), prq = bc(pr, I0{});
-  const double A0 = bc(p, I1{}), omA = bc(omp, I1{}), prA = bc(pr, I1{});
-  const double c0 = bc(p, I2{}), omc = bc(omp, I2{}), prc = bc(pr, I2{});
-  const double delta = bc(e, I3{});
-  const double phi = delta + 2.0;
-  const bool pmd = pt[0].pmd;
-  const double A = pmd ? A0 : 0.0, c = pmd ? c0 : 0.0;
-  double lprior = prq + v[3] - delta * 1e-3;
-  if (pmd) lprior += prA + prc;
-
-  // the pad's lnGamma(0 + phi) pair: lane 7 (pair, forward half) or lane 15
-  const LG3 t3b = lg3<false, MDFIT_TLOG_NUTS>(pt[1].N + phi);
-  const bool src15 = whole || hi8;
-  const double t6l = src15 ? rowb<15>(t3b.l) : rowb<7>(t3b.l);
-  const double t6p = src15 ? rowb<15>(t3b.p) : rowb<7>(t3b.p);
-  double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-  bool bad_lane = pmd && A + c >= 1.0;
-#ifndef MDFIT_NUTS_PT_UNROLL
-#define MDFIT_NUTS_PT_UNROLL 2
-#endif
-#pragma unroll MDFIT_NUTS_PT_UNROLL
-  for (int pi = 0; pi < 2; ++pi) {
-    const PointData& pd = pt[pi];
-    double D, dq, dA;
-    if (pmd) {
-      const double w = powk(omq, pd.k);
-      D = fma(A, w, c);
-      dq = pd.k > 0 ? -A * (double)pd.k * (w * rcp(omq)) : 0.0;
-      dA = w;
-    } else {
-      D = q;
-      dq = 1.0;
-      dA = 0.0;
-    }
-    bad_lane = bad_lane || (pd.valid && !(D < 1.0));
-    const double a = D * phi, b = (1.0 - D) * phi;
-    const LG3 t1 = lg3<false, MDFIT_TLOG_NUTS>(pd.y + a);
-    const LG3 t4 = lg3<false, MDFIT_TLOG_NUTS>(a);
-    const double la = t1.l - t4.l, Pa = t1.p - t4.p;
-    const LG3 t2 = lg3<false, MDFIT_TLOG_NUTS>(pd.N - pd.y + b);
-    const LG3 t5 = lg3<false, MDFIT_TLOG_NUTS>(b);
-    const double lb = t2.l - t5.l, Pb = t2.p - t5.p;
-    const LG3 t3 = pi == 1 ? t3b : lg3<false, MDFIT_TLOG_NUTS>(pd.N + phi);
-    const double ell = (la + lb) - (t3.l - t6l);
-    const double lD = phi * (Pa - Pb);
-    const double lF = D * Pa + (1.0 - D) * Pb + (t6p - t3.p);
-    if (pd.valid) {
-      acc[0] += ell;
-      acc[1] += lD * dq;
-      acc[2] += lD * dA;
-      acc[3] += lD;
-      acc[4] += lF;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 5; ++j) {
-    const double s8 = gsum<8>(acc[j]);
-    acc[j] = whole ? s8 + dpp<0x140>(s8) : s8;  // row_mirror: the other half's sum
-  }
-  const unsigned long long bm = __ballot(bad_lane);
-  const int sh = (int)(threadIdx.x & (whole ? ~15 : ~7));
-  const bool bad = ((bm >> sh) & (whole ? 0xFFFFull : 0xFFull)) != 0ull;
-  Pot o;
-  o.U = -(acc[0] + lprior);
-  o.g[0] = -(acc[1] * (q * omq) + (2.0 - 5.0 * q));
-  o.g[1] = pmd ? -(acc[2] * (A * omA) + (2.0 - 5.0 * A)) : 0.0;
-  o.g[2] = pmd ? -(acc[3] * (c * omc) + (1.0 - 10.0 * c)) : 0.0;
-  o.g[3] = -(acc[4] * delta + (1.0 - delta * 1e-3));
-  if (bad || !isfinite(o.U)) {
-    o.U = INFINITY;
-    o.g[0] = o.g[1] = o.g[2] = o.g[3] = 0.0;
-  }
-  return o;
 }
 
 // ---------------------------------------------------------------------------
@@ -377,743 +188,24 @@ __device__ __forceinline__ void ckpt_idxs(int n, int* imin, int* imax) {
   *imin = mx - ns + 1;
 }
 
-__device__ __forceinline__ double logaddexp(double a, double b) {
-  const double m = fmax(a, b);
-  return m == -INFINITY ? -INFINITY : m + flog1p(exp(-fabs(a - b)));
-}
-
-__device__ __forceinline__ bool is_turning(bool pmd, const double invm[4], const double rl[4], const double rr[4],
-                                           const double rsum[4]) {
-  double dl = 0.0, dr = 0.0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (!active(pmd, j)) continue;
-    const double rs = rsum[j] - 0.5 * (rl[j] + rr[j]);
-    dl += invm[j] * rl[j] * rs;
-    dr += invm[j] * rr[j] * rs;
-  }
-  return dl <= 0.0 || dr <= 0.0;
-}
-
-__device__ __forceinline__ double kinetic(bool pmd, const double invm[4], const double r[4]) {
-  double k = 0.0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (active(pmd, j)) k += invm[j] * r[j] * r[j];
-  return 0.5 * k;
-}
-
-// cold per-chain state (one slot per 16-lane row; every lane of the row
-// writes the same values)
-struct RowState {
-  double lz[4], lr[4], lg[4];  // left end of the trajectory
-  double rz[4], rr[4], rg[4];  // right end
-  double tz[4], tg[4], tpe;    // proposal of the tree = the chain's current state
-  double sz[4], sg[4], spe;    // proposal of the subtree being built
-  double wmean[4], wm2[4];     // Welford (slow windows)
-};
-
-// hot per-chain state (row-uniform, in LDS: see nuts_chain_kernel)
-struct ChainState {
-  int mode;
-  bool whole, drained;
-  int64_t taxon;
-  int sub;
-  Stream st;
-  int it, attempt;
-  // dynamics
-  double pz[4], pr[4], pg[4];
-  double step, eps, e0;
-  double invm[4];
-  double isd[4];  // sqrt(1 / invm): the momentum scale, recomputed when invm changes
-  // step-size search
-  int f_call, f_m, f_last, f_dir;
-  // dual averaging, windows
-  double x_avg, g_avg, mu;
-  int t_da, widx, wn;
-  // tree
-  double t_w, t_rsum[4], t_acc, u_tr;
-  int t_n, t_depth, leaf_ctr, nleap;
-  bool t_turn, t_div, right;
-  // subtree (the kernel keeps s_w .. nmax and leaf_ctr in registers; the
-  // fields stay: removing them measurably changes the register allocation)
-  double s_w, s_rsum[4], s_acc;
-  int s_n, n_leaf, nmax;
-  bool s_div;
-  int ul_chunk;  // chunk of leaf uniforms in sul (-1: none)
-  // statistics of the kept iterations
-  double st_div, st_leap;
-  int nm_chunk;  // chunk of 4 iterations whose momenta are in snm (-1: none)
-};
-
-__device__ __forceinline__ void chain_init(ChainState& c) {
-  c.mode = 0;
-  c.whole = c.drained = false;
-  c.taxon = 0;
-  c.sub = 0;
-  c.st = make_stream(0, 0, 0);
-  c.it = c.attempt = 0;
-  for (int j = 0; j < 4; ++j) {
-    c.pz[j] = c.pr[j] = c.pg[j] = c.t_rsum[j] = c.s_rsum[j] = 0.0;
-    c.invm[j] = c.isd[j] = 1.0;
-  }
-  c.step = 0.0;
-  c.eps = 1.0;
-  c.e0 = 0.0;
-  c.f_call = c.f_m = c.f_last = c.f_dir = 0;
-  c.x_avg = c.g_avg = c.mu = 0.0;
-  c.t_da = c.widx = c.wn = 0;
-  c.t_w = c.t_acc = c.u_tr = 0.0;
-  c.t_n = c.t_depth = c.leaf_ctr = c.nleap = 0;
-  c.t_turn = c.t_div = false;
-  c.right = true;
-  c.s_w = c.s_acc = 0.0;
-  c.s_n = c.n_leaf = 0;
-  c.nmax = 1;
-  c.s_div = false;
-  c.ul_chunk = -1;
-  c.st_div = c.st_leap = 0.0;
-  c.nm_chunk = -1;
-}
-
 constexpr int kInit = 1, kFind = 2, kIter = 3, kDone = 4;
 
 // ---------------------------------------------------------------------------
-// chain kernel
+// chain kernel, component-distributed layout
 // ---------------------------------------------------------------------------
-// Chain layouts (template PPL = points per lane): a task group of 2 chain
-// slots runs one all-position chain (both slots hold identical state, their
-// sums added) or the forward / reverse pair of one model (a chain per slot).
-//   PPL 1: slot = a 16-lane DPP row, lane = position (lane 15 the pad);
-//          2 task groups / 4 chain slots per wave.
-//   PPL 2: slot = 8 lanes, two positions per lane (pair: |z|-1 = 2j, 2j+1;
-//          all-position: z = +-(j+1) on 16 lanes); 4 task groups / 8 chain
-//          slots per wave -- every state-machine pass serves twice the chains.
-#ifndef MDFIT_NUTS_WAVES_PER_EU
-#define MDFIT_NUTS_WAVES_PER_EU 3  // PPL 1 register budget per lane: 512 / waves (VGPR+AGPR); 3 measured best (C3)
-#endif
-#ifndef MDFIT_NUTS_WAVES_PER_EU2
-#define MDFIT_NUTS_WAVES_PER_EU2 2  // PPL 2 (LDS: ~13.5 KB of chain state per wave)
-#endif
-#ifndef MDFIT_NUTS_PPL
-#define MDFIT_NUTS_PPL 1
-#endif
-template <int PPL>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PPL == 1 ? MDFIT_NUTS_WAVES_PER_EU : MDFIT_NUTS_WAVES_PER_EU2))) void nuts_chain_kernel(const uint32_t* __restrict__ gy,
-                                                           const uint32_t* __restrict__ gN, int64_t T,
-                                                           mdfit_opts o, double* __restrict__ out,
-                                                           int* __restrict__ ws, double* __restrict__ samples) {
-  static_assert(PPL == 1 || PPL == 2, "points per lane");
-  constexpr int kG = PPL == 1 ? 16 : 8;  // lanes per chain slot
-  constexpr int kNSlot = kWave / kG;     // chain slots per wave
-  constexpr int kTaskL = 2 * kG;         // lanes per task group
-  constexpr unsigned long long kTaskMask = kTaskL == 32 ? 0xFFFFFFFFull : 0xFFFFull;
-  constexpr unsigned long long kSlotMask = kG == 16 ? 0xFFFFull : 0xFFull;
-  __shared__ RowState srow[kNSlot];
-  __shared__ ChainState schain[kNSlot];
-  __shared__ double sck[8][kWave];  // checkpoint i of a slot on its lane i: r[4], rsum[4]
-  __shared__ double sck8[PPL == 2 ? kNSlot : 1][8];  // PPL 2: checkpoint 8 of a slot
-  // draws of the current iteration computed in parallel, 16 per slot (16 / kG
-  // per lane): entry j holds doubling j's direction bit and subtree-merge
-  // uniform, and leaf uniform 16 c + j of the current chunk c
-  // (ChainState::ul_chunk)
-  __shared__ double sut[16 * kNSlot], sul[16 * kNSlot];
-  // momenta of 4 iterations: entry e of a slot holds component e & 3 of
-  // iteration 4 c + (e >> 2), c = ChainState::nm_chunk
-  __shared__ double snm[16 * kNSlot];
-  __shared__ int sdb[16 * kNSlot];
-  const int lane = threadIdx.x;
-  const int r = lane & (kTaskL - 1), h = r / kG, i = r & (kG - 1), row = lane / kG;
-  const int row16 = row * 16;  // the slot's 16 entries of the draw caches
-  const int leader = lane & ~(kTaskL - 1);
-  const int qi = blockIdx.x % kQueues;
-  // queue qi owns the taxa [tl, tl + nq) and serves their 4 nq tasks heaviest
-  // kind first: PMD all-position chains, PMD fwd/rev pairs, null all-position,
-  // null pairs (every XCD gets the same mix; long chains start early)
-  const int64_t tl = T * qi / kQueues, nq = T * (qi + 1) / kQueues - tl;
-  const int W = o.num_warmup, S = o.num_samples;
-  RowState& R = srow[row];
-  ChainState& C = schain[row];
-
-  PointData pd[PPL];
-#pragma unroll
-  for (int p = 0; p < PPL; ++p) {
-    pd[p].valid = PPL == 1 ? i < kNHalf : 0;
-    pd[p].k = PPL == 1 && i < kNHalf ? i : 0;
-    pd[p].y = pd[p].N = 0.0;
-    pd[p].pmd = true;
-  }
-
-  // The chain state is row-uniform (every lane of a row holds the same values;
-  // both rows of an all-position chain too) and lives in LDS, so the
-  // potential's registers are what bounds occupancy.
-  int& mode = C.mode;  // 0 idle, kInit, kFind, kIter, kDone
-  bool& whole = C.whole;
-  bool& drained = C.drained;
-  int64_t& taxon = C.taxon;
-  int& sub = C.sub;
-  Stream& st = C.st;
-  int& it = C.it;
-  int& attempt = C.attempt;
-  double* pz = C.pz;
-  double* pr = C.pr;
-  double* pg = C.pg;
-  double& step = C.step;
-  double& eps = C.eps;
-  double& e0 = C.e0;
-  double* invm = C.invm;
-  double* isd = C.isd;
-  int& f_call = C.f_call;
-  int& f_m = C.f_m;
-  int& f_last = C.f_last;
-  int& f_dir = C.f_dir;
-  double& x_avg = C.x_avg;
-  double& g_avg = C.g_avg;
-  double& mu = C.mu;
-  int& t_da = C.t_da;
-  int& widx = C.widx;
-  int& wn = C.wn;
-  double& t_w = C.t_w;
-  double* t_rsum = C.t_rsum;
-  double& t_acc = C.t_acc;
-  double& u_tr = C.u_tr;
-  int& t_n = C.t_n;
-  int& t_depth = C.t_depth;
-  int leaf_ctr = 0;
-  int& nleap = C.nleap;
-  bool& t_turn = C.t_turn;
-  bool& t_div = C.t_div;
-  bool& right = C.right;
-  int& ul_chunk = C.ul_chunk;
-  // the subtree being built: touched by every leaf, so kept in registers
-  // (row-uniform like the LDS state; A/B: -3.5 % chain time at C3)
-  double s_w = 0.0, s_rsum[4] = {0, 0, 0, 0}, s_acc = 0.0;
-  int s_n = 0, n_leaf = 0, nmax = 1;
-  bool& s_div = C.s_div;
-  double& st_div = C.st_div;
-  double& st_leap = C.st_leap;
-  chain_init(C);  // every lane of the row writes the same values
-  for (int j = 0; j < 8; ++j) sck[j][lane] = 0.0;
-  if (PPL == 2 && i == 0)
-    for (int j = 0; j < 8; ++j) sck8[row][j] = 0.0;
-  // the adaptation schedule depends on num_warmup only: window ends once per
-  // wave (lane w < 16 resolves window w) instead of once per transition
-  __shared__ int swin_end[kMaxWin];
-  __shared__ int swin_n;
-  if (lane < kMaxWin) {
-    int e, n;
-    windows(W, lane, &e, &n);
-    swin_end[lane] = e;
-    if (lane == 0) swin_n = n;
-  }
-  __syncthreads();
-#ifdef MDFIT_STAMP
-  // stamp k (set by whichever lanes reach point k; 0 = not reached this trip)
-  // opens section k: 0 task start, 1 potential, 2 mode dispatch up to the leaf
-  // weights, 5 checkpoints + U-turn checks, 6 subtree merge, 7 transition end
-  // (adaptation / draw), 8 rest of the dispatch, 3 begin probe / iteration,
-  // 4 loop tail.  acc_t[k]: cycles per section, acc_t[9]: trips
-  constexpr int kNStamp = 10;
-  __shared__ unsigned long long sstamp[kNStamp];
-  unsigned long long acc_t[kNStamp] = {};
-  const unsigned long long t_begin = nstamp();
-  sstamp[0] = 0;
-#endif
-
-  while (true) {
-#ifdef MDFIT_STAMP
-    {
-      const unsigned long long now = nstamp();
-      if (sstamp[0] != 0) {  // book the previous trip, sections in program order
-        constexpr int order[9] = {0, 1, 2, 5, 6, 7, 8, 3, 4};
-        int cur = 0;
-        unsigned long long last = sstamp[0];
-        // (acc_t indexed by literals only: a runtime index would put it in
-        // scratch and charge global-memory round trips to the task start)
-#pragma unroll
-        for (int j = 1; j < 9; ++j) {
-          const int k = order[j];
-          if (sstamp[k] == 0) continue;
-          const unsigned long long d = sstamp[k] - last;
-#pragma unroll
-          for (int q = 0; q < 9; ++q)
-            if (q == cur) acc_t[q] += d;
-          last = sstamp[k];
-          cur = k;
-        }
-#pragma unroll
-        for (int q = 0; q < 9; ++q)
-          if (q == cur) acc_t[q] += now - last;
-        acc_t[9] += 1;
-      }
-      sstamp[0] = now;
-      for (int j = 1; j < kNStamp; ++j) sstamp[j] = 0;
-    }
-#endif
-    // ---- 1. free groups start a task (one atomic per wave-trip) --------------
-    const unsigned long long busy_m = __ballot(mode != 0 && mode != kDone);
-    const bool group_free = ((busy_m >> leader) & kTaskMask) == 0ull;
-    if (group_free) mode = 0;  // both chains finished (or none started)
-    const bool need = group_free && !drained;
-    bool starting = false;
-    if (__any(need)) {
-      const unsigned long long m = __ballot(need && r == 0);
-      int base = 0;
-      if (lane == 0) base = atomicAdd(ws + qi, __popcll(m));
-      base = __shfl(base, 0);
-      if (need) {
-        const int64_t task = (int64_t)base + __popcll(m & ((1ull << leader) - 1ull));
-        if (task >= 4 * nq) {
-          drained = true;
-          mode = 0;
-        } else {
-          const int kind = (int)(task / nq);
-          taxon = tl + task % nq;
-          whole = kind == 0 || kind == 2;
-          sub = kind == 0 ? 0 : (kind == 2 ? 1 : (kind == 1 ? 2 : 4) + h);
-          starting = true;
-        }
-      }
-    }
-    if (starting) {
-      const int pmd_task = sub == 0 || sub == 2 || sub == 3;
-#pragma unroll
-      for (int p = 0; p < PPL; ++p) {
-        pd[p].pmd = pmd_task;
-        int colv;
-        if (PPL == 1) {
-          // row h reads columns h*15 + k: the two halves of an all-position
-          // chain, or the forward (sub 2 / 4) / reverse (sub 3 / 5) chain of a pair
-          colv = h * kNHalf + pd[p].k;
-        } else if (whole) {  // lane r: z = +(r+1) (p 0) and -(r+1) (p 1)
-          pd[p].valid = r < kNHalf;
-          pd[p].k = r < kNHalf ? r : 0;
-          colv = p * kNHalf + pd[p].k;
-        } else {  // lane i of half h: |z|-1 = 2i + p of direction h
-          pd[p].valid = 2 * i + p < kNHalf;
-          pd[p].k = pd[p].valid ? 2 * i + p : 0;
-          colv = h * kNHalf + pd[p].k;
-        }
-        pd[p].y = pd[p].valid ? (double)gy[taxon * kLD + colv] : 0.0;
-        pd[p].N = pd[p].valid ? (double)gN[taxon * kLD + colv] : 0.0;
-      }
-      st = make_stream(o.seed, o.index_base + taxon, sub);
-      C.nm_chunk = -1;
-      // fresh chain state (oracle: nuts_chain)
-      mode = kInit;
-      attempt = 0;
-      it = 0;
-      st_div = st_leap = 0.0;
-      eps = 1.0;
-      step = 0.0;
-      f_call = f_m = f_last = f_dir = 0;
-      x_avg = g_avg = mu = 0.0;
-      t_da = widx = wn = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pz[j] = active(pd[0].pmd, j) ? -2.0 + 4.0 * uniform(st, 0xFFFF0000u, (uint32_t)j) : 0.0;
-        pr[j] = pg[j] = 0.0;
-        invm[j] = isd[j] = 1.0;
-        R.wmean[j] = R.wm2[j] = 0.0;
-      }
-    }
-    if (!__any(mode != 0 || !drained)) break;
-    NSTAMP(1);
-    const bool running = mode == kInit || mode == kFind || mode == kIter;
-    if (!__any(running)) continue;  // (only finished chains of unfinished groups)
-
-    // ---- 2. one evaluation: the initial point, or a leapfrog step ------------
-    double rh[4], zev[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      rh[j] = pr[j] - 0.5 * step * pg[j];
-      zev[j] = mode == kInit ? pz[j] : pz[j] + step * invm[j] * rh[j];
-    }
-#ifdef MDFIT_NUTS_POT_TWICE  // development: marginal cost of one potential evaluation
-    double zev2[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) zev2[j] = zev[j] * (1.0 + 1e-300 * (double)it);
-    const Pot P0 = PPL == 1 ? potential(pd[0], zev2, whole) : potential2(pd, zev2, whole);
-    Pot P = PPL == 1 ? potential(pd[0], zev, whole) : potential2(pd, zev, whole);
-    P.U += 0.0 * P0.U * (double)(it > (1 << 30));
-#else
-    const Pot P = PPL == 1 ? potential(pd[0], zev, whole) : potential2(pd, zev, whole);
-#endif
-    NSTAMP(2);
-    if (!running) continue;
-    double rn[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      rn[j] = rh[j] - 0.5 * step * P.g[j];
-      pz[j] = zev[j];
-    }
-
-    bool begin_iter = false, begin_find = false;
-    if (mode == kInit) {
-      if (isfinite(P.U)) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          R.tz[j] = zev[j];
-          R.tg[j] = P.g[j];
-        }
-        R.tpe = P.U;
-        eps = 1.0;
-        f_call = 0;
-        begin_find = true;
-      } else if (++attempt >= 100) {
-        // no finite initial point: NaN draws, status 2
-        for (int s = i; s < S; s += kG)
-          if (!whole || h == 0)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              samples[((taxon * MDFIT_NSUBFIT + sub) * (int64_t)S + s) * 4 + j] = NAN;
-        if ((!whole || h == 0) && i < 4) {
-          double* dg = out + taxon * MDFIT_NOUT + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * sub;
-          dg[4 + i] = i == 2 ? (double)MDFIT_NONFINITE : NAN;
-        }
-        mode = kDone;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          pz[j] = active(pd[0].pmd, j) ? -2.0 + 4.0 * uniform(st, 0xFFFF0000u + (uint32_t)attempt, (uint32_t)j) : 0.0;
-      }
-    } else if (mode == kFind) {
-      const double de = (P.U + kinetic(pd[0].pmd, invm, rn)) - e0;
-      const int dnew = log(kTarget) < -de ? 1 : -1;
-      f_last = f_dir;
-      f_dir = dnew;
-      ++f_m;
-      const bool cont = (eps > kTiny || f_dir >= 0) && (eps < kHuge || f_dir <= 0) &&
-                        (f_last == 0 || f_dir == f_last) && f_m < 4000;
-      if (cont) {
-        begin_find = true;  // next probe of the same search
-      } else {
-        mu = log(10.0 * eps);
-        x_avg = g_avg = 0.0;
-        t_da = 0;
-        begin_iter = true;
-      }
-    } else {  // kIter: a leaf of the subtree
-      ++nleap;
-      double de = (P.U + kinetic(pd[0].pmd, invm, rn)) - e0;
-      if (isnan(de)) de = INFINITY;
-      const double w = -de;
-      const bool dv = de > kMaxDelta;
-      const double acc = de > 0.0 ? exp(-de) : 1.0;
-      if (n_leaf == 0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          R.sz[j] = zev[j];
-          R.sg[j] = P.g[j];
-          s_rsum[j] = rn[j];
-        }
-        R.spe = P.U;
-        s_w = w;
-        s_acc = acc;
-        s_n = 1;
-      } else {
-        // nw = logaddexp(s_w, w) and prob = exp(w - nw) from one exp:
-        // prob = 1 / (1 + e^(s_w - w)) (or e/(1+e) when w < s_w)
-        const double m = fmax(s_w, w);
-        const double e = exp(-fabs(s_w - w));
-        const double nw = m == -INFINITY ? -INFINITY : m + flog1p(e);
-        const double prob = (w >= s_w ? 1.0 : e) * rcp(1.0 + e);
-        if ((leaf_ctr >> 4) != ul_chunk) {  // next 16 leaf uniforms, 16 / kG per lane
-#pragma unroll
-          for (int e2 = 0; e2 < 16 / kG; ++e2) {
-            const int ix = i + kG * e2;
-            sul[row16 + ix] = uniform(st, (uint32_t)it, 32u + (uint32_t)(leaf_ctr & ~15) + (uint32_t)ix);
-          }
-          ul_chunk = leaf_ctr >> 4;
-        }
-        if (sul[row16 + (leaf_ctr & 15)] < prob) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            R.sz[j] = zev[j];
-            R.sg[j] = P.g[j];
-          }
-          R.spe = P.U;
-        }
-        s_w = nw;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) s_rsum[j] += rn[j];
-        s_acc += acc;
-        s_n += 1;
-      }
-      NSTAMP(5);
-      s_div = dv;
-      ++leaf_ctr;
-      int imin, imax;
-      ckpt_idxs(n_leaf, &imin, &imax);
-      // checkpoint ix (0..8) on lane ix of the slot (PPL 2: checkpoint 8 in
-      // sck8, lane 0)
-      if ((n_leaf & 1) == 0 && i == imax) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          sck[j][lane] = rn[j];
-          sck[4 + j][lane] = s_rsum[j];
-        }
-      }
-      if (PPL == 2 && (n_leaf & 1) == 0 && imax == 8 && i == 0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          sck8[row][j] = rn[j];
-          sck8[row][4 + j] = s_rsum[j];
-        }
-      }
-      bool my_turn = false;
-      if (i >= imin && i <= imax) {
-        double ck_r[4], sub_rsum[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          ck_r[j] = sck[j][lane];
-          sub_rsum[j] = s_rsum[j] - sck[4 + j][lane] + ck_r[j];
-        }
-        my_turn = is_turning(pd[0].pmd, invm, ck_r, rn, sub_rsum);
-      }
-      if (PPL == 2 && i == 0 && imin <= 8 && imax >= 8) {
-        double ck_r[4], sub_rsum[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          ck_r[j] = sck8[row][j];
-          sub_rsum[j] = s_rsum[j] - sck8[row][4 + j] + ck_r[j];
-        }
-        my_turn = my_turn || is_turning(pd[0].pmd, invm, ck_r, rn, sub_rsum);
-      }
-      const unsigned long long tm = __ballot(my_turn);
-      const bool s_turn = ((tm >> (lane & ~(kG - 1))) & kSlotMask) != 0ull;
-      ++n_leaf;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) pr[j] = rn[j];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) pg[j] = P.g[j];
-      NSTAMP(6);
-      if (s_turn || s_div || n_leaf == nmax) {
-        // merge the subtree into the tree: biased progressive sampling
-        // prob = min(1, exp(s_w - t_w)) and t_w' = logaddexp(t_w, s_w) from one
-        // exp: for s_w <= t_w, exp(s_w - t_w) = exp(-|t_w - s_w|)
-        const double em = exp(-fabs(t_w - s_w));
-        const double prob = (s_turn || s_div) ? 0.0 : (s_w > t_w ? 1.0 : em);
-        if (u_tr < prob) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            R.tz[j] = R.sz[j];
-            R.tg[j] = R.sg[j];
-          }
-          R.tpe = R.spe;
-        }
-        double olr[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          olr[j] = right ? R.lr[j] : R.rr[j];  // r of the untouched end
-          if (right) {
-            R.rz[j] = pz[j];
-            R.rr[j] = pr[j];
-            R.rg[j] = pg[j];
-          } else {
-            R.lz[j] = pz[j];
-            R.lr[j] = pr[j];
-            R.lg[j] = pg[j];
-          }
-        }
-        {
-          const double m = fmax(t_w, s_w);
-          t_w = m == -INFINITY ? -INFINITY : m + flog1p(em);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) t_rsum[j] += s_rsum[j];
-        t_turn = s_turn || (right ? is_turning(pd[0].pmd, invm, olr, pr, t_rsum) : is_turning(pd[0].pmd, invm, pr, olr, t_rsum));
-        t_div = s_div;
-        t_acc += s_acc;
-        t_n += s_n;
-        ++t_depth;
-        if (t_depth >= kMaxDepth || t_turn || t_div) {
-          NSTAMP(7);
-          // ---- the transition is complete: adapt or keep the draw ----------
-          const double accp = t_acc / (double)t_n;
-          if (it < W) {
-            ++t_da;
-            const double gg = kTarget - accp;
-            const double inv = 1.0 / (t_da + 10.0);
-            g_avg = (1.0 - inv) * g_avg + gg * inv;
-            const double x_t = mu - sqrt((double)t_da) * 20.0 * g_avg;  // / gamma (0.05)
-            const double sq = sqrt((double)t_da);
-            const double wt = 1.0 / (sq * sqrt(sq));  // t^-0.75
-            x_avg = (1.0 - wt) * x_avg + wt * x_t;
-            eps = exp(it == W - 1 ? x_avg : x_t);
-            if (eps < kTiny) eps = kTiny;
-            const int wend = widx < kMaxWin ? swin_end[widx] : -1, nwin = swin_n;
-            const bool middle = widx > 0 && widx < nwin - 1;
-            if (middle) {
-              ++wn;
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                if (!active(pd[0].pmd, j)) continue;
-                const double d0 = R.tz[j] - R.wmean[j];
-                R.wmean[j] += d0 / wn;
-                R.wm2[j] += d0 * (R.tz[j] - R.wmean[j]);
-              }
-            }
-            const bool at_end = it == wend;
-            if (at_end && middle) {
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                if (!active(pd[0].pmd, j)) continue;
-                const double var = R.wm2[j] / (wn - 1);
-                invm[j] = ((double)wn / (wn + 5.0)) * var + 1e-3 * (5.0 / (wn + 5.0));
-                isd[j] = sqrt(1.0 / invm[j]);
-                R.wmean[j] = R.wm2[j] = 0.0;
-              }
-              wn = 0;
-              ++f_call;
-              begin_find = true;
-            }
-            if (at_end) ++widx;
-          } else {
-            const int64_t sidx = ((taxon * MDFIT_NSUBFIT + sub) * (int64_t)S + (it - W)) * 4;
-            if ((!whole || h == 0) && i < 4) {
-              const double zj = R.tz[i];
-              samples[sidx + i] = i == 3 ? exp(zj) + 2.0
-                                         : ((i == 0 || pd[0].pmd) ? 1.0 / (1.0 + exp(-zj)) : 0.0);
-            }
-            st_div += t_div ? 1.0 : 0.0;
-            st_leap += (double)nleap;
-          }
-          ++it;
-          if (it == W + S) {
-            if ((!whole || h == 0) && i < 4) {
-              double* dg = out + taxon * MDFIT_NOUT + MDFIT_F_DIAG + MDFIT_DIAG_STRIDE * sub;
-              dg[4 + i] = i == 0 ? eps : (i == 1 ? st_leap / S : (i == 2 ? (double)MDFIT_OK : st_div));
-            }
-            mode = kDone;
-          } else if (!begin_find) {
-            begin_iter = true;
-          }
-          NSTAMP(8);
-        } else {
-          // next doubling
-          const int j = t_depth;
-          right = sdb[row16 + j] != 0;
-          u_tr = sut[row16 + j];
-          n_leaf = 0;
-          nmax = 1 << j;
-          step = right ? eps : -eps;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            pz[k] = right ? R.rz[k] : R.lz[k];
-            pr[k] = right ? R.rr[k] : R.lr[k];
-            pg[k] = right ? R.rg[k] : R.lg[k];
-          }
-        }
-      } else {
-        step = right ? eps : -eps;  // next leaf of the subtree continues from (pz, pr, pg)
-      }
-    }
-
-    NSTAMP(3);
-    if (begin_find) {
-      // one probe of find_reasonable_step_size from the current state
-      if (mode != kFind || f_m == 0) {
-        f_m = 0;
-        f_last = f_dir = 0;
-      }
-      if (mode != kFind) mode = kFind;
-      eps = ldexp(eps, f_dir);
-      // the 4 momentum draws in parallel: lane j of the row draws component j
-      double nj[4];
-      slot4<kG>(normal(st, 0xFFFE0000u + 4096u * (uint32_t)f_call + (uint32_t)f_m, (uint32_t)(i & 3)), nj);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pr[j] = active(pd[0].pmd, j) ? nj[j] * isd[j] : 0.0;
-        pz[j] = R.tz[j];
-        pg[j] = R.tg[j];
-      }
-      e0 = R.tpe + kinetic(pd[0].pmd, invm, pr);
-      step = eps;
-    }
-    if (begin_iter) {
-      mode = kIter;
-      // this iteration's momenta from the 4-iteration cache (the same draws,
-      // keyed by iteration and component; one Box-Muller pass per 4 iterations)
-      if ((it >> 2) != C.nm_chunk) {
-#pragma unroll
-        for (int e2 = 0; e2 < 16 / kG; ++e2) {
-          const int ix = i + kG * e2;
-          snm[row16 + ix] = normal(st, (uint32_t)((it & ~3) + (ix >> 2)), (uint32_t)(ix & 3));
-        }
-        C.nm_chunk = it >> 2;
-      }
-      double nj[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) nj[j] = snm[row16 + 4 * (it & 3) + j];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pr[j] = active(pd[0].pmd, j) ? nj[j] * isd[j] : 0.0;
-        pz[j] = R.tz[j];
-        pg[j] = R.tg[j];
-        R.lz[j] = R.rz[j] = pz[j];
-        R.lr[j] = R.rr[j] = pr[j];
-        R.lg[j] = R.rg[j] = pg[j];
-        t_rsum[j] = pr[j];
-      }
-      e0 = R.tpe + kinetic(pd[0].pmd, invm, pr);
-      t_w = 0.0;
-      t_acc = 0.0;
-      t_n = 0;
-      t_depth = 0;
-      t_turn = t_div = false;
-      leaf_ctr = 0;
-      nleap = 0;
-      // this iteration's doubling draws, lane j of the row for depth j
-#pragma unroll
-      for (int e2 = 0; e2 < 16 / kG; ++e2) {
-        const int ix = i + kG * e2;
-        sdb[row16 + ix] = (int)(block(st, (uint32_t)it, 4u + 2u * (uint32_t)ix).x & 1u);
-        sut[row16 + ix] = uniform(st, (uint32_t)it, 5u + 2u * (uint32_t)ix);
-      }
-      ul_chunk = -1;
-      right = sdb[row16] != 0;
-      u_tr = sut[row16];
-      n_leaf = 0;
-      nmax = 1;
-      step = right ? eps : -eps;
-    }
-    NSTAMP(4);
-  }
-#ifdef MDFIT_STAMP
-  if (lane == 0 && g_nuts_stamp) {
-    unsigned long long* w = g_nuts_stamp + 16 * (size_t)blockIdx.x;
-    for (int j = 0; j < kNStamp; ++j) w[j] = acc_t[j];
-    w[10] = nstamp() - t_begin;
-  }
-#endif
-}
-
-// ---------------------------------------------------------------------------
-// chain kernel, component-distributed layout (MDFIT_NUTS_CD, the default)
-// ---------------------------------------------------------------------------
-// The slots, tasks, Philox draws and state machine of nuts_chain_kernel, with
-// the chain's 4-vectors (position, momentum, gradient, inverse mass, momentum
-// sums, the trajectory ends and proposals) held one component per lane: lane i
-// of a slot holds component i & 3 (the slot's quads hold copies).  A leapfrog
-// is then 3 instructions instead of 12, a vector costs 2 VGPRs instead of 8, and
-// the hot chain state (dynamics, subtree, tree, step size, counters) lives in
-// registers instead of LDS; the cold vectors (trajectory ends, proposals,
-// Welford) are per-slot LDS arrays of 4.  Dot products (kinetic energy,
-// U-turn criteria) gather the four components and add them in the oracle's
-// order without contraction (oracle/mdfit_nuts.c: kinetic, is_turning).
-#ifndef MDFIT_NUTS_CD
-#define MDFIT_NUTS_CD 1
-#endif
-#ifndef MDFIT_POST_NRM_INLINE
-#define MDFIT_POST_NRM_INLINE 1  // the post kernel's gamma draws call an inlined normal
-#endif
-#ifndef MDFIT_POST_U32
-#define MDFIT_POST_U32 1  // post kernel: the draws' counts sorted (4 B each) and a one-pass WAIC: 4 KB of LDS instead of 8
-#endif
-#ifndef MDFIT_NUTS_STEAL
-#define MDFIT_NUTS_STEAL 1  // chain waves take tasks from the other XCDs' queues once theirs runs dry
-#endif
+// A 16-lane slot runs one chain; a task group of two slots runs one
+// all-position chain (both slots hold identical state, their sums added) or the
+// forward / reverse pair of one model (a chain per slot).  The chain's
+// 4-vectors (position, momentum, gradient, inverse mass, momentum sums, the
+// trajectory ends and proposals) are held one component per lane: lane i of a
+// slot holds component i & 3 (the slot's quads hold copies).  A leapfrog is
+// then 3 instructions, a vector costs 2 VGPRs, and the hot chain state
+// (dynamics, subtree, step size, counters) lives in registers; the cold vectors
+// (trajectory ends, proposals, Welford) are per-slot LDS arrays of 4.  Dot
+// products (kinetic energy, U-turn criteria) gather the four components and
+// add them in the oracle's order without contraction (oracle/mdfit_nuts.c:
+// kinetic, is_turning).  A wave serves its XCD's task queue, then the other
+// queues in turn once that one runs dry.
 // a wave whose chain has run long takes issue priority over its SIMD's other
 // waves (s_setprio 1 / 2 / 3 past 32k / 64k / 128k wave-trips since the chain
 // started): the kernel ends with its longest chain (C3: 2-4.5e5 trips, ~15 us
@@ -1121,9 +213,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(PPL == 1 
 // critical path; checked every 256 trips
 #ifndef MDFIT_NUTS_PRIO
 #define MDFIT_NUTS_PRIO 1
-#endif
-#ifndef MDFIT_NUTS_COLD_LEAF
-#define MDFIT_NUTS_COLD_LEAF 1
 #endif
 #ifndef MDFIT_NUTS_PRIO_T
 #define MDFIT_NUTS_PRIO_T 32768.0  // trips of the first level (x2, x4 for the next)
@@ -1143,9 +232,11 @@ struct PotC {
   double g;  // this lane's component of the gradient
 };
 
-// The potential of `potential` / `potential2` with the input and the gradient
-// component-distributed: every lane resolves its own component (c < 3:
-// sigmoid, c == 3: exp), lanes 0-3 of the slot are broadcast.
+// -(log density + log|J|) of the slot's (or, `whole`, the task group's) points
+// at x and its gradient (oracle: nuts_potential), with the input and the
+// gradient component-distributed: every lane resolves its own component (c < 3:
+// sigmoid, c == 3: exp), lanes 0-3 of the slot are broadcast; the phi pair is
+// the pad lane's lg(0 + phi).
 template <int PPL>
 __device__ __forceinline__ PotC potential_cd(const PointData pt[PPL], double x, bool whole, bool run = true) {
   constexpr int kG = PPL == 1 ? 16 : 8;
@@ -1343,7 +434,7 @@ struct ColdState {
   int sub, attempt, f_call, f_m, f_last, f_dir, t_da, widx, wn, nm_chunk;
   int t_n, t_depth;
   double t_start;  // the wave's trip count when the chain started (MDFIT_NUTS_PRIO)
-  double s_acc;    // (MDFIT_NUTS_COLD_LEAF) the subtree's acceptance sum,
+  double s_acc;    // the subtree's acceptance sum,
   int s_n, ul_chunk;  // size and the chunk of leaf uniforms in sul
 #ifdef MDFIT_DEV_TRIPS  // development: per-chain start / end clock and trips in diag 4, 5, 7
   double dev_t0, dev_c0;
@@ -1381,7 +472,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   ColdState& C = scold[row];                                                              \
   (void)h, (void)c, (void)row16, (void)leader, (void)V, (void)C
   MDFIT_CD_LAYOUT(threadIdx.x);
-  // a wave serves its XCD's queue, then (MDFIT_NUTS_STEAL) the next queues in
+  // a wave serves its XCD's queue, then the next queues in
   // turn once that one runs dry: the chains are ~1e4 trips long, so the last
   // ones started decide the kernel's end (which wave runs a chain changes no
   // draw: the streams are keyed by taxon and sub-fit)
@@ -1422,7 +513,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   }
   __syncthreads();
 #ifdef MDFIT_STAMP
-  // the sections of nuts_chain_kernel's split (see there)
+  // the split's sections: the time from each NSTAMP(k) to the next stamp
+  // reached (their names: tools/nuts_stamp_profile.py)
   constexpr int kNStamp = 10;
   __shared__ unsigned long long sstamp[kNStamp];
   unsigned long long acc_t[kNStamp] = {};
@@ -1437,7 +529,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   // (the tree's scalars -- weight, acceptance sum, size, depth, merge uniform --
   // and the step size are touched once per doubling: ColdState)
   double step = 0.0, e0 = 0.0;
-#if MDFIT_NUTS_COLD_LEAF
   // (the subtree's acceptance sum and size and the leaf-uniform chunk live in
   // the row's ColdState: touched once a leaf, they were the kernel's spills)
   double s_w = 0.0;
@@ -1445,16 +536,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   C.s_acc = 0.0;
   C.s_n = 0;
   C.ul_chunk = -1;
-#define MDFIT_CD_SACC C.s_acc
-#define MDFIT_CD_SN C.s_n
-#define MDFIT_CD_ULC C.ul_chunk
-#else
-  double s_w = 0.0, s_acc = 0.0;
-  int leaf_ctr = 0, nleap = 0, s_n = 0, n_leaf = 0, nmax = 1, ul_chunk = -1;
-#define MDFIT_CD_SACC s_acc
-#define MDFIT_CD_SN s_n
-#define MDFIT_CD_ULC ul_chunk
-#endif
   int right = 1, t_turn = 0, t_div = 0, s_div = 0;
 // slot utilisation and the point-evaluation count (bench.py's compute
 // roofline): wave-trips with a running slot, and running slot-trips (each one
@@ -1514,7 +595,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       if (need) {
         const int64_t task = (int64_t)base + __popcll(m & ((1ull << leader) - 1ull));
         if (task >= 4 * nq) {
-          drained = !MDFIT_NUTS_STEAL || qs + 1 >= kQueues ? 1 : 0;  // (else: the next queue next trip)
+          drained = qs + 1 >= kQueues ? 1 : 0;  // (else: the next queue next trip)
           mode = 0;
         } else {
           const int kind = (int)(task / nq);
@@ -1524,7 +605,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
           starting = true;
         }
       }
-      if (MDFIT_NUTS_STEAL && dry && qs + 1 < kQueues) {
+      if (dry && qs + 1 < kQueues) {
         ++qs;
         qi = (qi + 1) % kQueues;
         tl = T * qi / kQueues;
@@ -1697,20 +778,20 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         C.spe = P.U;
         V[kVss][c] = rn;
         s_w = w;
-        MDFIT_CD_SACC = acc;
-        MDFIT_CD_SN = 1;
+        C.s_acc = acc;
+        C.s_n = 1;
       } else {
         const double m = fmax(s_w, w);
         const double e = exp(-fabs(s_w - w));
         const double nw = m == -INFINITY ? -INFINITY : m + lae1p(e);
         const double prob = (w >= s_w ? 1.0 : e) * rcp(1.0 + e);
-        if ((leaf_ctr >> 4) != MDFIT_CD_ULC) {  // next 16 leaf uniforms, 16 / kG per lane
+        if ((leaf_ctr >> 4) != C.ul_chunk) {  // next 16 leaf uniforms, 16 / kG per lane
 #pragma unroll
           for (int e2 = 0; e2 < 16 / kG; ++e2) {
             const int ix = i + kG * e2;
             sul[row16 + ix] = uniform(C.st, (uint32_t)it, 32u + (uint32_t)(leaf_ctr & ~15) + (uint32_t)ix);
           }
-          MDFIT_CD_ULC = leaf_ctr >> 4;
+          C.ul_chunk = leaf_ctr >> 4;
         }
         if (sul[row16 + (leaf_ctr & 15)] < prob) {
           V[kVsz][c] = zev;
@@ -1719,8 +800,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         }
         s_w = nw;
         V[kVss][c] += rn;
-        MDFIT_CD_SACC += acc;
-        MDFIT_CD_SN += 1;
+        C.s_acc += acc;
+        C.s_n += 1;
       }
       s_div = dv;
       ++leaf_ctr;
@@ -1798,8 +879,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         V[kVtr][c] = trs;
         t_turn = s_turn || (right ? turning_cd<kG>(act, im, olr, rm, trs) : turning_cd<kG>(act, im, rm, olr, trs));
         t_div = s_div;
-        C.t_acc += MDFIT_CD_SACC;
-        C.t_n += MDFIT_CD_SN;
+        C.t_acc += C.s_acc;
+        C.t_n += C.s_n;
         ++C.t_depth;
         if (C.t_depth >= kMaxDepth || t_turn || t_div) {
           NSTAMP(7);
@@ -1946,7 +1027,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         if (ix < 8) sdb[row16 + j] = (int)(b.x & 1u);
         else sut[row16 + j] = u53(b.x, b.y);
       }
-      MDFIT_CD_ULC = -1;
+      C.ul_chunk = -1;
       right = sdb[row16] != 0;
       C.u_tr = sut[row16];
       n_leaf = 0;
@@ -1955,9 +1036,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
     }
     NSTAMP(4);
   }
-#undef MDFIT_CD_SACC
-#undef MDFIT_CD_SN
-#undef MDFIT_CD_ULC
 #ifdef MDFIT_STAMP
   if (lane == 0 && g_nuts_stamp) {
     unsigned long long* w = g_nuts_stamp + 16 * (size_t)blockIdx.x;
@@ -1981,7 +1059,7 @@ struct Draw {
   const Stream* st;
   uint32_t w2, w3;
   __device__ double uni() { return uniform(*st, w2, w3++); }
-  __device__ double nrm() { return MDFIT_POST_NRM_INLINE ? normal_inl(*st, w2, w3++) : normal(*st, w2, w3++); }
+  __device__ double nrm() { return normal_inl(*st, w2, w3++); }
 };
 
 __device__ double log_gamma_draw(Draw& d, double alpha) {
@@ -2050,21 +1128,17 @@ __device__ __forceinline__ double d_at(const double* th, bool pmd, int k) {
   return D < 0.0 ? 0.0 : (D > 1.0 ? 1.0 : D);
 }
 
-__device__ double predictive_frac(const Stream& st, int s, int col, int k, double Nn, const double* th) {
+// One predictive Beta-Binomial draw as its integer count obs <= N (the
+// oracle's predictive_frac is obs / N: the post kernel sorts the counts and
+// forms the fractions after).  A draw that is not a count in [0, N] (NaN theta
+// or p) returns -1: the oracle's NaN fraction makes median and HPDI NaN.
+__device__ int64_t predictive_count(const Stream& st, int s, int col, int k, double Nn, const double* th) {
   const double D = d_at(th, true, k);
   Draw d{&st, 0xFFFD0000u + (uint32_t)s, (uint32_t)col << 16};
   const double lx = log_gamma_draw(d, D * th[3]), ly = log_gamma_draw(d, (1.0 - D) * th[3]);
   const double p = 1.0 / (1.0 + exp(ly - lx));
-  return binomial_draw(d, Nn, p) / Nn;
-}
-
-// the draw itself (an integer count <= N): predictive_frac = predictive_count / N
-__device__ uint32_t predictive_count(const Stream& st, int s, int col, int k, double Nn, const double* th) {
-  const double D = d_at(th, true, k);
-  Draw d{&st, 0xFFFD0000u + (uint32_t)s, (uint32_t)col << 16};
-  const double lx = log_gamma_draw(d, D * th[3]), ly = log_gamma_draw(d, (1.0 - D) * th[3]);
-  const double p = 1.0 / (1.0 + exp(ly - lx));
-  return (uint32_t)binomial_draw(d, Nn, p);
+  const double obs = binomial_draw(d, Nn, p);
+  return (obs >= 0.0 && obs <= Nn) ? (int64_t)obs : -1;
 }
 
 // wave-wide reductions
@@ -2074,31 +1148,6 @@ __device__ __forceinline__ double wmax(double v) {
   return v;
 }
 
-// bitonic sort of n <= kMaxSamples doubles in LDS (n padded to a power of two with +inf)
-__device__ void lds_sort(double* v, int n) {
-  int m = 1;
-  while (m < n) m <<= 1;
-  for (int j = n + threadIdx.x; j < m; j += kWave) v[j] = INFINITY;
-  __syncthreads();
-  for (int k = 2; k <= m; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int x = threadIdx.x; x < m; x += kWave) {
-        const int y = x ^ j;
-        if (y > x) {
-          const double a = v[x], b = v[y];
-          const bool up = (x & k) == 0;
-          if ((a > b) == up) {
-            v[x] = b;
-            v[y] = a;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
-
-// np.median + numpyro hpdi(prob 0.68) of the S sorted values
 // bitonic sort of n counts in LDS (padded to a power of two with UINT32_MAX)
 __device__ void lds_sort_u32(uint32_t* v, int n) {
   int m = 1;
@@ -2122,10 +1171,10 @@ __device__ void lds_sort_u32(uint32_t* v, int n) {
     }
   }
 }
-// median_hpdi over the fractions c / N of sorted counts c: each fraction is
-// formed as predictive_frac forms it, so the result is median_hpdi's on the
-// sorted fractions bit for bit (c -> c / N is monotone: the same order, ties
-// where the fractions tie)
+// np.median + numpyro hpdi(prob 0.68) over the fractions c / N of the S sorted
+// counts c: each fraction is formed as the oracle's predictive_frac forms it,
+// so the result is its median_hpdi on the sorted fractions bit for bit
+// (c -> c / N is monotone: the same order, ties where the fractions tie)
 __device__ void median_hpdi_counts(const uint32_t* c, int S, double Nn, double out3[3]) {
   auto f = [&](int x) { return (double)c[x] / Nn; };
   out3[0] = (S & 1) ? f(S / 2) : 0.5 * (f(S / 2 - 1) + f(S / 2));
@@ -2150,30 +1199,6 @@ __device__ void median_hpdi_counts(const uint32_t* c, int S, double Nn, double o
   out3[1] = f(best);
   out3[2] = f(best + len);
 }
-__device__ void median_hpdi(const double* v, int S, double out3[3]) {
-  out3[0] = (S & 1) ? v[S / 2] : 0.5 * (v[S / 2 - 1] + v[S / 2]);
-  const int len = (int)(0.68 * S);
-  double bw = INFINITY;
-  int best = 0;
-  for (int x = threadIdx.x; x < S - len; x += kWave) {
-    const double w = v[x + len] - v[x];
-    if (w < bw) {  // first minimum per lane
-      bw = w;
-      best = x;
-    }
-  }
-  // wave argmin, ties -> lowest index
-  for (int o = 32; o >= 1; o >>= 1) {
-    const double ow = __shfl_xor(bw, o, 64);
-    const int ob = __shfl_xor(best, o, 64);
-    if (ow < bw || (ow == bw && ob < best)) {
-      bw = ow;
-      best = ob;
-    }
-  }
-  out3[1] = v[best];
-  out3[2] = v[best + len];
-}
 
 __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __restrict__ gy,
                                                           const uint32_t* __restrict__ gN,
@@ -2189,7 +1214,7 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
   // fixed kMaxSamples array made the block 37 KB and capped the kernel at one
   // wave per SIMD)
   extern __shared__ double s_v[];
-  uint32_t* s_c = reinterpret_cast<uint32_t*>(s_v);  // (MDFIT_POST_U32: the predictive draws' counts)
+  uint32_t* s_c = reinterpret_cast<uint32_t*>(s_v);  // the predictive draws' counts
   const int lane = threadIdx.x;
   const int64_t t = blockIdx.x;
   const int S = o.num_samples;
@@ -2237,18 +1262,13 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
   }
 
   // ---- waic_i per chain and point (fits.py:126-172), lanes over draws ----------
-#ifdef MDFIT_DEV_POST_NOWAIC  // development: timing split of the post kernel
-  for (int s = 0; s < 0; ++s) {
-#else
   for (int s = 0; s < MDFIT_NSUBFIT; ++s) {
-#endif
     const bool pmd = s == 0 || s == 2 || s == 3;
     const int lo = (s == 3 || s == 5) ? kNHalf : 0, hi = s < 2 ? kNPos : lo + kNHalf;
     for (int col = lo; col < hi; ++col) {
       const double yy = s_y[col], nn = s_N[col];
       const int k = col < kNHalf ? col : col - kNHalf;
       const double lc = lg3<false, MDFIT_TLOG_NUTS>(nn + 1.0).l - lg3<false, MDFIT_TLOG_NUTS>(yy + 1.0).l - lg3<false, MDFIT_TLOG_NUTS>(nn - yy + 1.0).l;
-#if MDFIT_POST_U32
       // one pass: per lane a running max with its sum of exp (log-sum-exp) and
       // Welford's mean / M2 over its draws, combined across the wave -- the
       // lppd and variance of the two passes, to rounding, with no per-draw store
@@ -2259,7 +1279,10 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
         const double a = D * phi, b = (1.0 - D) * phi;
         const double lp = lc + (lg3<false, MDFIT_TLOG_NUTS>(yy + a).l - lg3<false, MDFIT_TLOG_NUTS>(a).l) + (lg3<false, MDFIT_TLOG_NUTS>(nn - yy + b).l - lg3<false, MDFIT_TLOG_NUTS>(b).l) -
                           (lg3<false, MDFIT_TLOG_NUTS>(nn + phi).l - lg3<false, MDFIT_TLOG_NUTS>(a + b).l);
-        if (lp > mxl) {
+        if (lp == -INFINITY) {
+          // exp(lp - mx) = 0 for every mx: nothing to add (and with mxl still
+          // -inf the else branch would form exp(-inf + inf) = NaN)
+        } else if (lp > mxl) {
           sel = sel * exp(mxl - lp) + 1.0;
           mxl = lp;
         } else {
@@ -2275,28 +1298,6 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
       const double mean = wsum(cnt * mul) / S;
       const double dm = mul - mean;
       const double var = wsum(m2l + cnt * dm * dm) / S;
-#else
-      double mx = -INFINITY, sm = 0.0;
-      for (int x = lane; x < S; x += kWave) {
-        const double* th = smp + ((int64_t)s * S + x) * 4;
-        const double D = d_at(th, pmd, k), phi = th[3];
-        const double a = D * phi, b = (1.0 - D) * phi;
-        const double lp = lc + (lg3<false, MDFIT_TLOG_NUTS>(yy + a).l - lg3<false, MDFIT_TLOG_NUTS>(a).l) + (lg3<false, MDFIT_TLOG_NUTS>(nn - yy + b).l - lg3<false, MDFIT_TLOG_NUTS>(b).l) -
-                          (lg3<false, MDFIT_TLOG_NUTS>(nn + phi).l - lg3<false, MDFIT_TLOG_NUTS>(a + b).l);
-        s_v[x] = lp;
-        mx = fmax(mx, lp);
-        sm += lp;
-      }
-      mx = wmax(mx);
-      const double mean = wsum(sm) / S;
-      double se = 0.0, var = 0.0;
-      for (int x = lane; x < S; x += kWave) {
-        se += exp(s_v[x] - mx);
-        var += (s_v[x] - mean) * (s_v[x] - mean);
-      }
-      se = wsum(se);
-      var = wsum(var) / S;
-#endif
       const double lppd = mx + log(se) - log((double)S);
       if (lane == 0) s_waic[s][col] = -2.0 * (lppd - var);
       __syncthreads();
@@ -2367,27 +1368,19 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
       m3[0] = m3[1] = m3[2] = NAN;
     } else {
       const Stream st = make_stream(o.seed, o.index_base + t, s);
-#ifdef MDFIT_DEV_POST_NODRAW
-      for (int x = lane; x < S; x += kWave) s_v[x] = smp[((int64_t)s * S + x) * 4] * (double)(col + 1);
-      (void)s_c;
-#else
-#if MDFIT_POST_U32
-      for (int x = lane; x < S; x += kWave)
-        s_c[x] = predictive_count(st, x, col, k, nn, smp + ((int64_t)s * S + x) * 4);
-#else
-      for (int x = lane; x < S; x += kWave) s_v[x] = predictive_frac(st, x, col, k, nn, smp + ((int64_t)s * S + x) * 4);
-#endif
-#endif
+      bool bad = false;
+      for (int x = lane; x < S; x += kWave) {
+        const int64_t cnt = predictive_count(st, x, col, k, nn, smp + ((int64_t)s * S + x) * 4);
+        bad = bad || cnt < 0;
+        s_c[x] = (uint32_t)(cnt < 0 ? 0 : cnt);
+      }
       __syncthreads();
-#if MDFIT_POST_U32
-      lds_sort_u32(s_c, S);
-      median_hpdi_counts(s_c, S, nn, m3);
-#else
-#ifndef MDFIT_DEV_POST_NOSORT
-      lds_sort(s_v, S);
-#endif
-      median_hpdi(s_v, S, m3);
-#endif
+      if (__any(bad)) {  // (wave-uniform) the oracle: any NaN fraction -> NaN median and HPDI
+        m3[0] = m3[1] = m3[2] = NAN;
+      } else {
+        lds_sort_u32(s_c, S);
+        median_hpdi_counts(s_c, S, nn, m3);
+      }
       __syncthreads();
     }
     if (lane == 0) {
@@ -2430,59 +1423,20 @@ __global__ __launch_bounds__(kWave) void nuts_potential_kernel(const int32_t* __
   const int lane = threadIdx.x;
   const bool whole = subset[it] == 0;
   const int dir = subset[it] == 2 ? 1 : 0;
-  double v[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = gv[it * 4 + j];
-  Pot P;
-  if (MDFIT_NUTS_CD) {  // the component-distributed potential of nuts_chain_cd
-    constexpr int kP = MDFIT_NUTS_PPL;
-    PointData pd[kP];
-#pragma unroll
-    for (int p = 0; p < kP; ++p) {
-      const int k = kP == 1 ? (lane & 15) : (whole ? (lane & 15) : 2 * (lane & 7) + p);
-      const int hh = kP == 1 ? ((lane & 31) >> 4) : p;
-      pd[p].pmd = model[it] == 0;
-      pd[p].valid = (kP == 1 ? (whole ? lane < 32 : lane < 16) : (whole ? lane < 16 : lane < 8)) && k < kNHalf;
-      pd[p].k = pd[p].valid ? k : 0;
-      const int col = pd[p].valid ? (whole ? hh : dir) * kNHalf + k : 0;
-      pd[p].y = pd[p].valid ? (double)gy[it * kLD + col] : 0.0;
-      pd[p].N = pd[p].valid ? (double)gN[it * kLD + col] : 0.0;
-    }
-    const PotC pc = potential_cd<kP>(pd, v[lane & 3], whole);
-    if (lane < 4) {
-      if (lane == 0) U[it] = pc.U;
-      g[it * 4 + lane] = pc.g;
-    }
-    return;
-  }
-  if (MDFIT_NUTS_PPL == 1) {
-    const int r = lane & 31, h = r >> 4, k = r & 15;
-    PointData pd;
-    pd.pmd = model[it] == 0;
-    pd.valid = (whole ? lane < 32 : lane < 16) && k < kNHalf;
-    pd.k = pd.valid ? k : 0;
-    const int col = pd.valid ? (whole ? h : dir) * kNHalf + k : 0;
-    pd.y = pd.valid ? (double)gy[it * kLD + col] : 0.0;
-    pd.N = pd.valid ? (double)gN[it * kLD + col] : 0.0;
-    P = potential(pd, v, whole);
-  } else {  // the chain kernel's PPL 2 layout on lanes 0-15 (whole) or 0-7
-    PointData pd[2];
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      pd[p].pmd = model[it] == 0;
-      const int k = whole ? (lane & 15) : 2 * (lane & 7) + p;
-      pd[p].valid = (whole ? lane < 16 : lane < 8) && k < kNHalf;
-      pd[p].k = pd[p].valid ? k : 0;
-      const int col = pd[p].valid ? (whole ? p : dir) * kNHalf + k : 0;
-      pd[p].y = pd[p].valid ? (double)gy[it * kLD + col] : 0.0;
-      pd[p].N = pd[p].valid ? (double)gN[it * kLD + col] : 0.0;
-    }
-    P = potential2(pd, v, whole);
-  }
-  if (lane == 0) {
-    U[it] = P.U;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) g[it * 4 + j] = P.g[j];
+  // the component-distributed potential of nuts_chain_cd (PPL 1): lane k of a
+  // row = |z| - 1, rows 0 / 1 = forward / reverse (whole) or the subset's row
+  const int k = lane & 15, hh = (lane & 31) >> 4;
+  PointData pd[1];
+  pd[0].pmd = model[it] == 0;
+  pd[0].valid = (whole ? lane < 32 : lane < 16) && k < kNHalf;
+  pd[0].k = pd[0].valid ? k : 0;
+  const int col = pd[0].valid ? (whole ? hh : dir) * kNHalf + k : 0;
+  pd[0].y = pd[0].valid ? (double)gy[it * kLD + col] : 0.0;
+  pd[0].N = pd[0].valid ? (double)gN[it * kLD + col] : 0.0;
+  const PotC pc = potential_cd<1>(pd, gv[it * 4 + (lane & 3)], whole);
+  if (lane < 4) {
+    if (lane == 0) U[it] = pc.U;
+    g[it * 4 + lane] = pc.g;
   }
 }
 
@@ -2544,18 +1498,18 @@ int fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t 
   // diag slots 4..7 are written by the chains; zero the record first
   if (hipMemsetAsync(out, 0, (size_t)n_taxa * MDFIT_NOUT * sizeof(double), s) != hipSuccess)
     return host::check_launch("hipMemsetAsync(out)");
-  constexpr int kPPL = MDFIT_NUTS_PPL;
+  constexpr int kPPL = 1;  // (PPL 2, two points per lane: 0.91x at C3, DESIGN_HISTORY)
   // (MDFIT_DEV_PER_CU: waves per CU forced, development A/B; the chain
   // kernel's waves never wait on each other, so any grid drains)
   const char* force = std::getenv("MDFIT_DEV_PER_CU");
-  auto chain = MDFIT_NUTS_CD ? nuts_chain_cd<kPPL> : nuts_chain_kernel<kPPL>;
+  auto chain = nuts_chain_cd<kPPL>;
   const int64_t g = host::fit_grid(chain, 4 * n_taxa, kPPL == 1 ? 2 : 4, 0, force ? std::atoi(force) : 0);
   host::prof_mark(1, s);
   host::debug_poison(s);
   hipLaunchKernelGGL(chain, dim3((unsigned)g), dim3(kWave), 0, s, y, N, n_taxa, o, out, ws, samples);
-  if (int rc = host::check_launch("nuts_chain_kernel")) return rc;
+  if (int rc = host::check_launch("nuts_chain_cd")) return rc;
   host::prof_mark(2, s);
-  const size_t elt = MDFIT_POST_U32 ? sizeof(uint32_t) : sizeof(double);
+  const size_t elt = sizeof(uint32_t);
   size_t sv_bytes = elt;
   while (sv_bytes < (size_t)o.num_samples * elt) sv_bytes <<= 1;  // the sort pads to 2^k
   // (the noise's counts and scratch reuse it after the draws: 1440 + 512 B)

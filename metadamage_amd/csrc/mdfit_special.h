@@ -32,15 +32,11 @@ __device__ __forceinline__ double rcp(double x) {
 }
 // One Newton step (<= 10 ulp): for reciprocals that only scale series
 // corrections (lnGamma's Stirling terms, the shift sums of psi), where the
-// relative error stays < 3e-15 of the function (lg3's fast form; MDFIT_RCP1
-// forces it everywhere, development A/B).
+// relative error stays < 3e-15 of the function (lg3's fast form).
 __device__ __forceinline__ double rcp1(double x) {
   const double r = __builtin_amdgcn_rcp(x);
   return fma(fma(-x, r, 1.0), r, r);
 }
-#ifndef MDFIT_RCP1
-#define MDFIT_RCP1 0
-#endif
 
 // Natural log, <= ~1 ulp (the classic reduction x = 2^e (1+f), 1+f in
 // [sqrt(1/2), sqrt(2)), log(1+f) = f - hfsq + s (hfsq + R(s^2)), s = f/(2+f),
@@ -72,9 +68,6 @@ __device__ __forceinline__ double flog(double x) {
   return normal ? r : (x == 0.0 ? -INFINITY : (x == INFINITY ? x : NAN));
 }
 
-#ifndef MDFIT_TLOG_FIT
-#define MDFIT_TLOG_FIT 0  // the fit kernel's point evaluation: within +-1 % at C2 and 125k (A/B), so off
-#endif
 #ifndef MDFIT_TLOG_NUTS
 #define MDFIT_TLOG_NUTS 1  // the sampler's potential and WAIC: C3 chain + post ~7.0 -> 6.3 s (A/B)
 #endif
@@ -169,7 +162,8 @@ struct LG3 {
 // the series' reciprocals (1/x of the Stirling terms, the shift sum's 1/P) by
 // one Newton step (rcp1, <= 10 ulp: < 3e-15 of psi) -- for the sampler's
 // potential and WAIC (MDFIT_TLOG_NUTS: C3 6.6 -> 6.1 s); the MAP fit, HPDI and
-// record kernels keep the accurate form (MDFIT_TLOG_FIT off: no gain there).
+// record kernels keep the accurate form (the table log in the fit kernel was
+// within +-1 % at C2 and 125k and spilled its PPL 2 layout: DESIGN.md §9).
 template <bool kTri = true, bool kTab = false>
 __device__ __forceinline__ LG3 lg3(double x) {
 #pragma clang fp contract(off)  // (every fusion explicit: the same bits in every inlined instance)
@@ -187,13 +181,9 @@ __device__ __forceinline__ LG3 lg3(double x) {
     }
     xs = x + 10.0;
   }
-  const double r = (MDFIT_RCP1 || kTab) ? rcp1(xs) : rcp(xs);
+  const double r = kTab ? rcp1(xs) : rcp(xs);
   const double r2 = r * r;
-#ifdef MDFIT_DEV_FAKELOG  // development: timing bound of a cheaper log (WRONG results)
-  const double lx = (double)__builtin_amdgcn_logf((float)xs) * 0.6931471805599453;
-#else
   const double lx = kTab ? flog_t(xs) : flog(xs);
-#endif
   // lnGamma(xs) ~ (xs - 1/2) ln xs - xs + ln(2 pi)/2 + r (1/12 - r2 (1/360 - ...))
   double sl = fma(r2, -1.0 / 156.0, 691.0 / 360360.0);
   sl = fma(r2, -sl, 1.0 / 1188.0);
@@ -222,13 +212,9 @@ __device__ __forceinline__ LG3 lg3(double x) {
     Q = fma(r * r2, sq, fma(0.5, r2, r));
   }
   if (shift) {
-    const double iP = (MDFIT_RCP1 || kTab) ? rcp1(P) : rcp(P);
+    const double iP = kTab ? rcp1(P) : rcp(P);
     const double s1 = dP * iP;          // sum 1/(x+j)
-#ifdef MDFIT_DEV_FAKELOG
-    L -= (double)__builtin_amdgcn_logf((float)P) * 0.6931471805599453;
-#else
     L -= kTab ? flog_t<true>(P) : flog(P);
-#endif
     Ps -= s1;
     if (kTri) Q += fma(s1, s1, -(d2P * iP));  // sum 1/(x+j)^2
   }
