@@ -415,16 +415,17 @@ def main():
             "hpdi_deferred_items": int(fb.workspace[128:132].view(torch.int32).item() & ~0x40000000),
         }
         if world == 1 and b is not None:
-            line["host_to_host"] = host_to_host(engine, b, opts, dev, max(5, args.steps // 2))
+            line["host_to_host"] = host_to_host(engine, b, opts, dev, max(5, args.steps // 2), generate)
         if ranks is not None:
             from metadamage_amd.distributed import REC_BYTES
 
             line["per_rank"] = ranks
             # what the one gather moves into rank 0 per step: every peer's
-            # padded shard of 564-B records (25 result doubles, 90 prediction
-            # floats, the status)
+            # padded shard of 496-B records (8 count doubles, 17 result floats,
+            # 90 prediction floats, the status)
             line["gather_bytes_to_rank0"] = REC_BYTES * cap * (world - 1)
             line["gather_record_bytes"] = REC_BYTES
+            line["gather_model"] = gather_model(REC_BYTES * cap, world, ranks)
             line["per_rank_note"] = ("a step split into the fit call and the one gather by the wall clock, "
                                      "measured after the timed region (synchronised per phase)")
         if (world == 1 and workload == "c2" or workload == "c4" and world > 1) and not args.no_c4_base:
@@ -446,6 +447,23 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+XGMI_LINK_GBS = 153.0  # per direct GPU-GPU link of an MI355X node (7 links per GPU, the node's full mesh)
+
+
+def gather_model(bytes_per_peer: int, world: int, ranks) -> dict:
+    """Modelled time of the one gather next to the measured one: every peer's
+    shard crosses its own direct xGMI link to rank 0 at once (full mesh), so
+    the transfer takes bytes_per_peer / link bandwidth; rank 0's ingress is
+    (world - 1) links, never the bound at world <= 8."""
+    ms = bytes_per_peer / (XGMI_LINK_GBS * 1e9) * 1e3
+    meas = [r["gather_ms"] for r in ranks] if ranks else []
+    return {"bytes_per_peer": bytes_per_peer, "link_GBs": XGMI_LINK_GBS, "modelled_ms": round(ms, 4),
+            "measured_ms_max": max(meas) if meas else None,
+            "note": "one dist.gather of the packed records to rank 0 over RCCL: modelled = bytes per peer / one "
+            "xGMI link (the peers send on their own links in parallel); measured = wall clock of the gather call "
+            "after the fit, per rank (includes RCCL launch and the rank-0 receive)"}
 
 
 def nuts_probe_rate(engine, dev, stream) -> float:
@@ -503,35 +521,69 @@ def c3_nuts(engine, _lib, generate, dev, stream, args) -> dict:
     return line
 
 
-def host_to_host(engine, b, opts, dev, steps: int) -> dict:
-    """The product call (engine.HostStaging, as fits.fit_packed runs it) timed
-    from pinned host buffers to pinned host buffers: with the mismatch counts
-    shipped (the product: the noise columns come from the assembly kernel) and
-    without (y, N only; the noise from the host library, ingest.noise, timed
-    separately)."""
+def host_to_host(engine, b, opts, dev, steps: int, generate=None) -> dict:
+    """The product call (fits.fit_packed -> engine.fit_batch_host: the chunked
+    two-stream dispatch of engine.ChunkedFitter, chunking as its staging
+    plans it) timed from the pinned host buffers the pipeline packs into
+    (engine.PinnedPack) to pinned host outputs: H2D of y, N and the mismatch
+    counts, the fit, D2H of the 32 record columns, predictions and status,
+    synchronised per call -- at C2 (10k taxa) and at C4's per-GPU share (125k,
+    seed 3), each next to the device-resident call of the same taxa.  Also
+    the y, N-only variant (the noise from the host library, ingest.noise,
+    timed separately)."""
     import torch
 
     from metadamage_amd import ingest
 
-    T = b.n_taxa
     out = {}
-    for name, mm in (("mm_shipped", b.mm), ("y_N_only", None)):
-        stg = engine.HostStaging(T, device=dev, opts=opts, with_mm=mm is not None)
-        stg.run(b.y, b.N, mm, opts)  # warm
+    batches = [("c2_10k", b)]
+    if generate is not None:
+        batches.append(("c4_share_125k", generate(C4_SHARE, seed=3)))
+    for name, bb in batches:
+        T = bb.n_taxa
+        ty, tN, tm = engine.to_device_counts(bb.y, bb.N, bb.mm, device=dev)
+        fb = engine.alloc_outputs(T, device=dev, opts=opts)
+        for _ in range(2):
+            engine.fit_batch_device(ty, tN, tm, opts, fb)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for _ in range(steps):
-            stg.run(b.y, b.N, mm, opts)
-        dt = (time.perf_counter() - t0) / steps
-        out[name] = {"value": round(T / dt, 1), "ms_per_call": round(dt * 1e3, 4),
-                     "h2d_bytes_per_taxon": 256 + (1440 if mm is not None else 0), "d2h_bytes_per_taxon": 256 + 360 + 4}
+            engine.fit_batch_device(ty, tN, tm, opts, fb)
+        torch.cuda.synchronize(dev)
+        dev_dt = (time.perf_counter() - t0) / steps
+        del ty, tN, tm, fb
+        pp = engine.PinnedPack(T)
+        y, N, mm = pp.views(T)
+        y[:], N[:], mm[:] = bb.y, bb.N, bb.mm
+        entry = {"taxa": T, "device_resident_fits_s": round(T / dev_dt, 1), "device_resident_ms": round(dev_dt * 1e3, 4)}
+        for kind, use_mm in (("mm_shipped", True), ("y_N_only", False)):
+            with engine._STAGING_LOCK:
+                st = engine.staging(T, device=dev, opts=opts, with_mm=use_mm)
+                chunks = engine.plan_chunks(T, opts, chunk_taxa=st.chunk_cap)
+                run = lambda: st.run(y, N, mm if use_mm else None, opts, pinned=pp if use_mm else None,  # noqa: E731
+                                     chunks=chunks)
+                run()
+                run()
+                ts = []
+                for _ in range(steps):
+                    t0 = time.perf_counter()
+                    run()
+                    ts.append(time.perf_counter() - t0)
+            dt = float(np.median(ts))
+            entry[kind] = {"value": round(T / dt, 1), "ms_per_call": round(dt * 1e3, 4), "chunks": len(chunks),
+                           "frac_of_device_resident": round(dev_dt / dt, 3),
+                           "h2d_bytes_per_taxon": 256 + (1440 if use_mm else 0), "d2h_bytes_per_taxon": 256 + 360 + 4}
+        out[name] = entry
+        del pp
+        engine._STAGING.clear()
+        torch.cuda.empty_cache()
     t0 = time.perf_counter()
     ingest.noise(b.mm)
-    out["host_noise_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+    out["host_noise_ms_c2"] = round((time.perf_counter() - t0) * 1e3, 3)
     out["unit"] = "fits/s"
-    out["note"] = ("pinned host y,N (+mm) -> H2D -> fit -> D2H of the 32 record columns, predictions, status; "
-                   "stream-synchronised per call; the product ships mm (the host noise path costs more CPU than "
-                   "the PCIe it saves while the multi-file pipeline is host-bound, DESIGN.md 10)")
+    out["note"] = ("pinned host y,N (+mm) -> H2D -> fit -> D2H of the 32 record columns, predictions, status, "
+                   "median of the calls, each synchronised; chunks > 1: ChunkedFitter's two streams overlap one "
+                   "chunk's copies with the other's fit (DESIGN.md 10); the PCIe-inclusive rate is never `value`")
     return out
 
 

@@ -18,14 +18,22 @@ import numpy as np
 
 from . import _lib
 
-# One gathered per-taxon record: the 25 result columns of out
-# (f64[NRES_GATHER]) | pred f32[3*30] | status i32 = 564 bytes.  The record's
-# 7 reserved doubles and its 48 per-sub-fit diagnostic doubles stay on the
-# rank that fitted them (1004 bytes per taxon otherwise).
+# One gathered per-taxon record (496 bytes): the 25 result columns of out as
+# the frames store them -- the 8 count columns (N_z1_*, N_sum_*, y_sum_*) as
+# f64 (exact integers up to 2^53; the frames' uint32 range check runs on rank 0)
+# and the 17 others rounded to f32 on the device, as downcast_dataframe rounds
+# them (utils.py:329-356: make_df_fit_results writes them float32, so the
+# frames are bit-identical to a single-process run) -- | pred f32[3*30] |
+# status i32.  The record's 7 reserved doubles and its 48 per-sub-fit
+# diagnostic doubles stay on the rank that fitted them.
 NRES_GATHER = _lib.NRESULT
+INT_LO, INT_HI = 7, 15  # result columns N_z1_forward .. y_sum_total (include/mdfit.h: MDFIT_F_N_Z1_FORWARD ..)
+FLOAT_COLS = [j for j in range(NRES_GATHER) if not INT_LO <= j < INT_HI]
+REC_INT = (INT_HI - INT_LO) * 8
+REC_F32 = len(FLOAT_COLS) * 4
 REC_PRED = _lib.NPRED * _lib.NPOS * 4
-REC_RES = NRES_GATHER * 8
-REC_BYTES = REC_PRED + 4 + REC_RES
+REC_RES = REC_INT + REC_F32
+REC_BYTES = REC_RES + REC_PRED + 4
 REC_OUT = _lib.NOUT * 8  # the full record the kernel writes (rank-local)
 
 
@@ -48,9 +56,10 @@ def shard_capacity(n_taxa: int, world: int) -> int:
 class Records:
     """Rank-local result buffers of a shard of n taxa: `out` f64[n, NOUT] (the
     kernel's full record), and one uint8 gather buffer `buf` of n * REC_BYTES
-    bytes holding res f64[n, NRES_GATHER] | pred f32[n, 3, 30] | status i32[n].
-    The kernel writes pred and status in place; `stage()` copies the result
-    columns of out into res (one strided device copy) before the gather."""
+    bytes holding ints f64[n, 8] | floats f32[n, 17] | pred f32[n, 3, 30] |
+    status i32[n].  The kernel writes pred and status in place; `stage()`
+    copies the result columns of out into ints / floats (two strided device
+    copies, the second rounding to f32) before the gather."""
 
     def __init__(self, n: int, device):
         import torch
@@ -58,23 +67,36 @@ class Records:
         self.n = n
         self.out = torch.empty((n, _lib.NOUT), dtype=torch.float64, device=device)
         self.buf = torch.empty(n * REC_BYTES, dtype=torch.uint8, device=device)
-        self.pred, self.status, self.res = packed_views(self.buf, n)
+        self.pred, self.status, self.ints, self.floats = packed_views(self.buf, n)
+        self._fidx = torch.as_tensor(FLOAT_COLS, device=device)
 
     def stage(self):
-        self.res.copy_(self.out[:, :NRES_GATHER])
+        self.ints.copy_(self.out[:, INT_LO:INT_HI])
+        self.floats.copy_(self.out.index_select(1, self._fidx))  # (f64 -> f32: round to nearest even, as numpy)
         return self.buf
 
 
 def packed_views(buf, n: int):
-    """Views (pred[n, 3, 30] f32, status[n] i32, res[n, NRES_GATHER] f64) into
-    one uint8 gather buffer of n * REC_BYTES bytes laid out res | pred | status
-    (torch tensor; the f64 block first keeps it 8-byte aligned for any n)."""
-    o1 = n * REC_RES
-    o2 = o1 + n * REC_PRED
-    res = buf[:o1].view(dtype=_torch_dtype("float64")).view(n, NRES_GATHER)
-    pred = buf[o1:o2].view(dtype=_torch_dtype("float32")).view(n, _lib.NPRED, _lib.NPOS)
-    status = buf[o2 : o2 + 4 * n].view(dtype=_torch_dtype("int32"))
-    return pred, status, res
+    """Views (pred[n, 3, 30] f32, status[n] i32, ints[n, 8] f64, floats[n, 17]
+    f32) into one uint8 gather buffer of n * REC_BYTES bytes laid out ints |
+    floats | pred | status (torch tensor; the f64 block first keeps it 8-byte
+    aligned for any n)."""
+    o1 = n * REC_INT
+    o2 = o1 + n * REC_F32
+    o3 = o2 + n * REC_PRED
+    ints = buf[:o1].view(dtype=_torch_dtype("float64")).view(n, INT_HI - INT_LO)
+    floats = buf[o1:o2].view(dtype=_torch_dtype("float32")).view(n, len(FLOAT_COLS))
+    pred = buf[o2:o3].view(dtype=_torch_dtype("float32")).view(n, _lib.NPRED, _lib.NPOS)
+    status = buf[o3 : o3 + 4 * n].view(dtype=_torch_dtype("int32"))
+    return pred, status, ints, floats
+
+
+def round_like_gather(out: np.ndarray) -> np.ndarray:
+    """The 25 result columns of host records out[T, >= 25] as the gather
+    carries them (the 17 non-count columns rounded to f32), float64[T, 25]."""
+    o = np.array(out[:, :NRES_GATHER], dtype=np.float64)
+    o[:, FLOAT_COLS] = o[:, FLOAT_COLS].astype(np.float32).astype(np.float64)
+    return o
 
 
 def _torch_dtype(name):
@@ -211,8 +233,11 @@ def unpack_gathered(parts, n_taxa: int, world: int):
     for r, part in enumerate(parts):
         lo, hi = shard_range(n_taxa, r, world)
         n_cap = part.numel() // REC_BYTES
-        p, s, o = packed_views(part, n_cap)
-        outs.append(o[: hi - lo].numpy())
+        p, s, ints, floats = packed_views(part, n_cap)
+        o = np.empty((hi - lo, NRES_GATHER), np.float64)
+        o[:, INT_LO:INT_HI] = ints[: hi - lo].numpy()
+        o[:, FLOAT_COLS] = floats[: hi - lo].numpy()
+        outs.append(o)
         preds.append(p[: hi - lo].numpy())
         sts.append(s[: hi - lo].numpy())
     return np.concatenate(outs), np.concatenate(preds), np.concatenate(sts)

@@ -8,6 +8,7 @@ CPU fallback: without a GPU these functions raise.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -130,72 +131,217 @@ def fit_batch(y, N, mm=None, opts: _lib.MdfitOpts | None = None, device="cuda"):
     return res.out.cpu().numpy(), res.pred.cpu().numpy(), res.status.cpu().numpy()
 
 
-class HostStaging:
-    """Pinned host buffers + device tensors for host-to-host fits of up to
-    `capacity` taxa (the product call): y, N go up (256 B per taxon) and,
-    with_mm, the mismatch counts (1,440 B; without them the noise columns
-    come back NaN and ingest.noise computes them on the host); the 32 record
-    columns (25 results + 7 reserved), the predictions and the status come
-    back (652 B per taxon).  All copies are stream-ordered on `stream`."""
+# --------------------------------------------------------------------------
+# bounded-memory chunked dispatch (the reference's 1,000-taxon chunks,
+# fits.py:692-706, as device-memory-sized chunks on two streams)
+# --------------------------------------------------------------------------
+MAX_CALL_TAXA = 1 << 25  # mdfit_fit_batch's per-call limit (MAP: int32 position indices)
+N_SETS = 2  # device buffer sets in flight: chunk k+1's H2D (and fit) beside chunk k's fit and D2H
+_BUDGET_FRAC = 0.6  # default device budget of a staging: this fraction of the free device memory
 
-    def __init__(self, capacity: int, device="cuda", opts: _lib.MdfitOpts | None = None, with_pred: bool = True,
-                 with_mm: bool = True):
+
+def device_bytes(C: int, opts: _lib.MdfitOpts | None = None, with_mm: bool = True, with_pred: bool = True,
+                 dest_on_device: bool = False) -> int:
+    """Device bytes one buffer set of a C-taxon chunk takes: the inputs (y, N:
+    256 B; mm: 1,440 B), the outputs (record 640 B, predictions 360 B, status 4
+    B -- unless the chunk writes into the caller's device buffers) and the
+    call's workspace (mdfit_workspace_bytes: MAP ~48 B below 60k taxa and
+    ~4.9 KB from 60k, NUTS 6 x num_samples x 32 B, the draws)."""
+    C = int(C)
+    b = C * (2 * _lib.LD * 4 + (_lib.NPOS * _lib.NMM * 4 if with_mm else 0))
+    if not dest_on_device:
+        b += C * (_lib.NOUT * 8 + (_lib.NPRED * _lib.NPOS * 4 if with_pred else 0) + 4)
+    return b + workspace_bytes(C, opts)
+
+
+def plan_chunks(T: int, opts: _lib.MdfitOpts | None = None, budget_bytes: int | None = None, *,
+                chunk_taxa: int = 0, n_sets: int = N_SETS, with_mm: bool = True, with_pred: bool = True,
+                dest_on_device: bool = False) -> list[tuple[int, int]]:
+    """Split T taxa into near-equal contiguous chunks [lo, hi) such that n_sets
+    buffer sets of the largest chunk fit in budget_bytes (None: no memory
+    bound), no chunk exceeds the per-call limit (2^25 taxa) or chunk_taxa (> 0;
+    env MDFIT_CHUNK_TAXA when 0).  Taxa are independent and the sampler's
+    streams are keyed by the global taxon index (opts.index_base + lo), so any
+    split gives the records of one call bit for bit."""
+    T = int(T)
+    if T <= 0:
+        return []
+    cap = min(T, MAX_CALL_TAXA)
+    if chunk_taxa <= 0:
+        chunk_taxa = int(os.environ.get("MDFIT_CHUNK_TAXA", "0") or 0)
+    if chunk_taxa > 0:
+        cap = min(cap, int(chunk_taxa))
+    if budget_bytes is not None:
+        per = lambda c: n_sets * device_bytes(c, opts, with_mm, with_pred, dest_on_device)  # noqa: E731
+        if per(1) > budget_bytes:
+            raise _lib.MdfitError(f"device budget {budget_bytes} B below one taxon's {per(1)} B")
+        if per(cap) > budget_bytes:  # largest c with per(c) <= budget (per is monotone in c)
+            lo, hi = 1, cap
+            while lo < hi:
+                mid = (lo + hi + 1) // 2
+                if per(mid) <= budget_bytes:
+                    lo = mid
+                else:
+                    hi = mid - 1
+            cap = lo
+    n = -(-T // cap)
+    return [(T * i // n, T * (i + 1) // n) for i in range(n)]
+
+
+def default_budget(device) -> int:
+    """The device budget of a staging (bytes): MDFIT_DEVICE_BUDGET_GB, else
+    _BUDGET_FRAC of the device memory free now."""
+    torch = _torch()
+    env = os.environ.get("MDFIT_DEVICE_BUDGET_GB")
+    if env:
+        return int(float(env) * (1 << 30))
+    free, _total = torch.cuda.mem_get_info(torch.device(device))
+    return int(_BUDGET_FRAC * free)
+
+
+class _Set:
+    """One chunk's device buffers and the stream its copies and call run on."""
+
+    def __init__(self, torch, C: int, device, opts, with_pred: bool, with_mm: bool, dest_on_device: bool):
+        self.stream = torch.cuda.Stream(device=device)
+        self.d_y = torch.empty((C, _lib.LD), dtype=torch.int32, device=device)
+        self.d_N = torch.empty((C, _lib.LD), dtype=torch.int32, device=device)
+        self.d_mm = torch.empty((C, _lib.NPOS, _lib.NMM), dtype=torch.int32, device=device) if with_mm else None
+        self.res = None if dest_on_device else alloc_outputs(C, device=device, with_pred=with_pred, opts=opts)
+        self.ws = self.res.workspace if self.res is not None else alloc_workspace(C, device, opts)
+
+
+class ChunkedFitter:
+    """Host-to-device fits of any number of taxa in chunks of at most
+    `chunk_cap` taxa through N_SETS device buffer sets, each on its own stream:
+    chunk k runs H2D -> mdfit_fit_batch -> D2H on set k % N_SETS's stream, so
+    the copies of one chunk overlap the fit of the other and consecutive fits
+    overlap each other's tails.  Device memory is N_SETS x device_bytes(chunk_cap)
+    whatever the batch size (the reference handles any number of taxa in
+    1,000-taxon chunks, fits.py:692-706; one call per file had a capacity cliff:
+    the NUTS draws are 192 KB per taxon, ~1.4M taxa per GPU).
+
+    Outputs go to pinned host buffers (run: the 32 record columns, the
+    predictions, the status; grown as needed and reused) or, run_into_device,
+    straight into the caller's device tensors (the sharded fit's gather
+    records)."""
+
+    def __init__(self, chunk_cap: int, device="cuda", opts: _lib.MdfitOpts | None = None, with_pred: bool = True,
+                 with_mm: bool = True, dest_on_device: bool = False):
         torch = _torch()
-        self.capacity = int(capacity)
+        self.chunk_cap = int(chunk_cap)
         self.device = torch.device(device)
-        T = self.capacity
-        self.h_y = torch.empty((T, _lib.LD), dtype=torch.int32).pin_memory()
-        self.h_N = torch.empty((T, _lib.LD), dtype=torch.int32).pin_memory()
-        self.h_mm = torch.empty((T, _lib.NPOS, _lib.NMM), dtype=torch.int32).pin_memory() if with_mm else None
-        self.h_out = torch.empty((T, 32), dtype=torch.float64).pin_memory()
-        self.h_pred = torch.empty((T, _lib.NPRED, _lib.NPOS), dtype=torch.float32).pin_memory() if with_pred else None
-        self.h_status = torch.empty((T,), dtype=torch.int32).pin_memory()
-        self.d_y = torch.empty((T, _lib.LD), dtype=torch.int32, device=self.device)
-        self.d_N = torch.empty((T, _lib.LD), dtype=torch.int32, device=self.device)
-        self.d_mm = torch.empty((T, _lib.NPOS, _lib.NMM), dtype=torch.int32, device=self.device) if with_mm else None
-        self.res = alloc_outputs(T, device=self.device, with_pred=with_pred, opts=opts)
+        self.with_pred, self.with_mm, self.dest_on_device = with_pred, with_mm, dest_on_device
+        self.sets = [_Set(torch, self.chunk_cap, self.device, opts, with_pred, with_mm, dest_on_device)
+                     for _ in range(N_SETS)]
+        self.full_cap = False  # (staging: the chunk capacity is the device budget's, not the batch's)
+        self.capacity = 0  # pinned host buffers (input staging for pageable sources, outputs)
+        self.h_y = self.h_N = self.h_mm = self.h_out = self.h_pred = self.h_status = None
 
-    def run(self, y, N, mm=None, opts: _lib.MdfitOpts | None = None, stream=None, sync: bool = True,
-            pinned: PinnedPack | None = None):
-        """Fit the first len(y) taxa; returns numpy views (out[:, :32], pred,
-        status) of the pinned buffers (valid until the next run).  pinned: y,
-        N, mm are that PinnedPack's views, copied to the device from there."""
+    def _host(self, T: int):
+        if T <= self.capacity:
+            return
         torch = _torch()
+        cap = int(1.25 * T) + 1
+        self.h_y = torch.empty((cap, _lib.LD), dtype=torch.int32).pin_memory()
+        self.h_N = torch.empty((cap, _lib.LD), dtype=torch.int32).pin_memory()
+        self.h_mm = torch.empty((cap, _lib.NPOS, _lib.NMM), dtype=torch.int32).pin_memory() if self.with_mm else None
+        if not self.dest_on_device:
+            self.h_out = torch.empty((cap, 32), dtype=torch.float64).pin_memory()
+            self.h_pred = (torch.empty((cap, _lib.NPRED, _lib.NPOS), dtype=torch.float32).pin_memory()
+                           if self.with_pred else None)
+            self.h_status = torch.empty((cap,), dtype=torch.int32).pin_memory()
+        self.capacity = cap
+
+    def _sources(self, y, N, mm, pinned):
+        """Pinned int32 views of the inputs: the PinnedPack's, or a copy into
+        the staging's own pinned buffers (H2D from pageable memory would be a
+        synchronous staged copy)."""
         T = int(y.shape[0])
-        if T > self.capacity:
-            raise ValueError(f"{T} taxa > staging capacity {self.capacity}")
-        use_mm = mm is not None and self.h_mm is not None
+        use_mm = mm is not None and self.with_mm
         if pinned is not None:
-            src_y, src_N, src_mm = pinned.h_y[:T], pinned.h_N[:T], pinned.h_mm[:T]
-        else:
-            self.h_y[:T].numpy()[:] = np.asarray(y, dtype=np.uint32).view(np.int32)
-            self.h_N[:T].numpy()[:] = np.asarray(N, dtype=np.uint32).view(np.int32)
-            if use_mm:
-                self.h_mm[:T].numpy()[:] = np.asarray(mm, dtype=np.uint32).view(np.int32)
-            src_y, src_N, src_mm = self.h_y[:T], self.h_N[:T], self.h_mm[:T] if use_mm else None
-        s = stream if stream is not None else torch.cuda.current_stream(self.device)
-        with torch.cuda.stream(s):
-            self.d_y[:T].copy_(src_y, non_blocking=True)
-            self.d_N[:T].copy_(src_N, non_blocking=True)
-            if use_mm:
-                self.d_mm[:T].copy_(src_mm, non_blocking=True)
-            res = FitBatch(self.res.out[:T], self.res.pred[:T] if self.res.pred is not None else None,
-                           self.res.status[:T], self.res.workspace)
-            fit_batch_device(self.d_y[:T], self.d_N[:T], self.d_mm[:T] if use_mm else None, opts, res, stream=s)
-            self.h_out[:T].copy_(res.out[:, :32], non_blocking=True)
-            if res.pred is not None:
-                self.h_pred[:T].copy_(res.pred, non_blocking=True)
-            self.h_status[:T].copy_(res.status, non_blocking=True)
+            return pinned.h_y[:T], pinned.h_N[:T], pinned.h_mm[:T] if use_mm else None
+        self._host(T)
+        self.h_y[:T].numpy()[:] = np.asarray(y, dtype=np.uint32).view(np.int32)
+        self.h_N[:T].numpy()[:] = np.asarray(N, dtype=np.uint32).view(np.int32)
+        if use_mm:
+            self.h_mm[:T].numpy()[:] = np.asarray(mm, dtype=np.uint32).view(np.int32)
+        return self.h_y[:T], self.h_N[:T], self.h_mm[:T] if use_mm else None
+
+    def _launch(self, chunks, src, opts, dest=None):
+        """Enqueue every chunk (asynchronous); returns the sets' streams."""
+        torch = _torch()
+        o0 = opts if opts is not None else _lib.default_opts()
+        src_y, src_N, src_mm = src
+        start = torch.cuda.Event()
+        start.record(torch.cuda.current_stream(self.device))  # after the caller's prior work
+        for k, (lo, hi) in enumerate(chunks):
+            st = self.sets[k % N_SETS]
+            n = hi - lo
+            o = _lib.MdfitOpts.from_buffer_copy(o0)
+            o.index_base = o0.index_base + lo  # the sampler's streams: global taxon index
+            st.stream.wait_event(start)
+            with torch.cuda.stream(st.stream):
+                st.d_y[:n].copy_(src_y[lo:hi], non_blocking=True)
+                st.d_N[:n].copy_(src_N[lo:hi], non_blocking=True)
+                if src_mm is not None:
+                    st.d_mm[:n].copy_(src_mm[lo:hi], non_blocking=True)
+                tm = st.d_mm[:n] if src_mm is not None else None
+                if dest is not None:
+                    res = FitBatch(dest.out[lo:hi], dest.pred[lo:hi] if dest.pred is not None else None,
+                                   dest.status[lo:hi], st.ws)
+                else:
+                    res = FitBatch(st.res.out[:n], st.res.pred[:n] if st.res.pred is not None else None,
+                                   st.res.status[:n], st.ws)
+                fit_batch_device(st.d_y[:n], st.d_N[:n], tm, o, res, stream=st.stream)
+                st.ws = res.workspace
+                if dest is None:
+                    self.h_out[lo:hi].copy_(res.out[:, :32], non_blocking=True)
+                    if res.pred is not None:
+                        self.h_pred[lo:hi].copy_(res.pred, non_blocking=True)
+                    self.h_status[lo:hi].copy_(res.status, non_blocking=True)
+        return [st.stream for st in self.sets]
+
+    def run(self, y, N, mm=None, opts: _lib.MdfitOpts | None = None, sync: bool = True,
+            pinned: PinnedPack | None = None, chunks=None):
+        """Fit len(y) taxa; returns numpy views (out[:, :32], pred, status) of the
+        pinned buffers (valid until the next run).  pinned: y, N, mm are that
+        PinnedPack's views.  chunks: the split (default plan_chunks at this
+        staging's chunk_cap)."""
+        T = int(y.shape[0])
+        if chunks is None:
+            chunks = plan_chunks(T, opts, chunk_taxa=self.chunk_cap)
+        if chunks and max(hi - lo for lo, hi in chunks) > self.chunk_cap:
+            raise ValueError(f"a chunk exceeds this staging's {self.chunk_cap} taxa")
+        self._host(T)
+        streams = self._launch(chunks, self._sources(y, N, mm, pinned), opts)
         if sync:
-            s.synchronize()
+            for s in streams:
+                s.synchronize()
         pred = self.h_pred[:T].numpy() if self.h_pred is not None else None
         return self.h_out[:T].numpy(), pred, self.h_status[:T].numpy()
+
+    def run_into_device(self, y, N, mm, opts, dest: FitBatch, chunks=None):
+        """Fit len(y) taxa chunk by chunk into the caller's device tensors dest
+        (out[T, NOUT], pred, status: rows written in place); stream-ordered
+        before the caller's current stream (which waits for every chunk)."""
+        torch = _torch()
+        T = int(y.shape[0])
+        if chunks is None:
+            chunks = plan_chunks(T, opts, chunk_taxa=self.chunk_cap)
+        streams = self._launch(chunks, self._sources(y, N, mm, None), opts, dest=dest)
+        cur = torch.cuda.current_stream(self.device)
+        for s in streams:
+            ev = torch.cuda.Event()
+            ev.record(s)
+            cur.wait_event(ev)
+        return dest
 
 
 class PinnedPack:
     """A pinned host buffer set for one file's packed counts (y, N: uint32
     [cap][32], mm: uint32[cap][30][12]): fits.pack_counts writes into it on a
-    reader thread and HostStaging.run copies it to the device directly (no
+    reader thread and ChunkedFitter.run copies it to the device directly (no
     host copy into the staging buffers: ~170 MB per 100k-taxon file)."""
 
     def __init__(self, capacity: int):
@@ -249,45 +395,60 @@ _STAGING: dict = {}
 _STAGING_LOCK = __import__("threading").Lock()
 
 
-def staging(capacity: int, device="cuda", opts: _lib.MdfitOpts | None = None, with_mm: bool = True) -> HostStaging:
-    """A HostStaging of at least `capacity` taxa, reused across calls of this
-    process (per device and buffer set): the multi-file pipeline fits one file
-    after another, and pinned + device buffers of ~2.3 KB (+ the ~4.8 KB MAP
-    workspace) per taxon allocated per file cost more host time than the fit.
-    Sized with x1.25 headroom, grown when a larger batch comes; fit_batch_host holds
+def staging(n_taxa: int, device="cuda", opts: _lib.MdfitOpts | None = None, with_mm: bool = True,
+            dest_on_device: bool = False, budget_bytes: int | None = None) -> ChunkedFitter:
+    """The ChunkedFitter for batches of n_taxa on this device, reused across calls
+    of this process (per device, buffer kind and sampler length): the
+    multi-file pipeline fits one file after another, and pinned + device
+    buffers allocated per file cost more host time than the fit.  Its chunk
+    capacity is the largest chunk N_SETS buffer sets of which fit the device
+    budget (default_budget), or n_taxa (x1.25 headroom) when smaller; a larger
+    batch than the chunk capacity is split into chunks (plan_chunks), so the
+    device memory it takes is bounded whatever the batch size.  Callers hold
     _STAGING_LOCK around its use (concurrent host threads take turns)."""
     torch = _torch()
     dev = torch.device(device)
     if dev.index is None:
         dev = torch.device(dev.type, torch.cuda.current_device())
     o = opts if opts is not None else _lib.default_opts()
-    key = (str(dev), bool(with_mm), int(o.mode), int(o.num_samples))
+    env_chunk = int(os.environ.get("MDFIT_CHUNK_TAXA", "0") or 0)
+    key = (str(dev), bool(with_mm), bool(dest_on_device), int(o.mode), int(o.num_samples), env_chunk)
     st = _STAGING.get(key)
-    if st is None or st.capacity < capacity:
-        _STAGING.pop(key, None)
-        # x1.25 headroom from the first allocation on: the files of a run
-        # differ in taxon count by a few %, and a regrow (pinned + device
-        # buffers, ~0.15 s at 100k taxa) costs more than the spare memory
-        cap = int(1.25 * max(int(capacity), st.capacity if st is not None else 0))
-        # (but not across the library's stream / after-the-fit HPDI switch: from
-        # 60k taxa the MAP workspace holds every position's wide-window record,
-        # ~4.8 KB per taxon that batches below 60k never touch)
-        if int(capacity) < _lib.STREAM_MAX_TAXA:
-            cap = min(cap, _lib.STREAM_MAX_TAXA - 1)
-        st = HostStaging(cap, device=dev, opts=o, with_mm=with_mm)
-        _STAGING[key] = st
+    T = max(1, int(n_taxa))
+    if st is not None and (st.chunk_cap >= T or st.full_cap):
+        return st
+    _STAGING.pop(key, None)
+    del st
+    budget = budget_bytes if budget_bytes is not None else default_budget(dev)
+    # the largest chunk the budget allows (x1.25 headroom over this batch: the
+    # files of a run differ in taxon count by a few %)
+    want = int(1.25 * T) + 1
+    # (not across the library's stream / after-the-fit HPDI switch: from 60k
+    # taxa the MAP workspace holds every position's wide-window record, ~4.8 KB
+    # per taxon that batches below 60k never touch)
+    if T < _lib.STREAM_MAX_TAXA:
+        want = min(want, _lib.STREAM_MAX_TAXA - 1)
+    cap = plan_chunks(want, o, budget, chunk_taxa=env_chunk, with_mm=with_mm, dest_on_device=dest_on_device)[0]
+    cap = cap[1] - cap[0]
+    st = ChunkedFitter(cap, device=dev, opts=o, with_mm=with_mm, dest_on_device=dest_on_device)
+    # (chunk capacity below the batch: memory-bound, no regrow for larger batches)
+    st.full_cap = cap < want
+    _STAGING[key] = st
     return st
 
 
 def fit_batch_host(y, N, mm=None, opts: _lib.MdfitOpts | None = None, noise=None, device="cuda",
                    pinned: PinnedPack | None = None):
-    """The product's host-to-host fit: (out[T, 32], pred, status).  mm goes
-    to the device (the assembly computes the noise columns); without it,
-    `noise` (float64[T][3], ingest.noise) fills them when given.  pinned: y,
-    N, mm are views of that PinnedPack (copied to the device from there)."""
+    """The product's host-to-host fit: (out[T, 32], pred, status), chunked
+    through the device budget (ChunkedFitter).  mm goes to the device (the
+    assembly computes the noise columns); without it, `noise` (float64[T][3],
+    ingest.noise) fills them when given.  pinned: y, N, mm are views of that
+    PinnedPack (copied to the device from there)."""
+    T = int(np.asarray(y).shape[0])
     with _STAGING_LOCK:
-        st = staging(int(np.asarray(y).shape[0]), device=device, opts=opts, with_mm=mm is not None)
-        out, pred, status = st.run(y, N, mm, opts, pinned=pinned if mm is not None else None)
+        st = staging(T, device=device, opts=opts, with_mm=mm is not None)
+        out, pred, status = st.run(y, N, mm, opts, pinned=pinned if mm is not None else None,
+                                   chunks=plan_chunks(T, opts, chunk_taxa=st.chunk_cap))
         out, pred, status = out.copy(), pred.copy(), status.copy()
     if mm is None and noise is not None:
         ok = status != _lib.INVALID

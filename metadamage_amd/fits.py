@@ -241,12 +241,14 @@ def _fit_sharded(p: Packed, opts, dev, rank: int, world: int):
     cap = shard_capacity(p.n_taxa, world)
     rec = alloc_records(cap, dev)
     if hi > lo:
-        ty, tN, tm = engine.to_device_counts(p.y[lo:hi], p.N[lo:hi], p.mm[lo:hi] if p.mm is not None else None,
-                                             device=dev)
-    p.release_pinned()  # (to_device_counts copied synchronously)
-    if hi > lo:
-        engine.fit_batch_device(ty, tN, tm, opts, engine.FitBatch(rec.out[: hi - lo], rec.pred[: hi - lo],
-                                                                   rec.status[: hi - lo]))
+        # the shard through the bounded-memory chunked dispatch, each chunk's
+        # records written in place into the gather buffers
+        with engine._STAGING_LOCK:
+            st = engine.staging(hi - lo, device=dev, opts=opts, with_mm=p.mm is not None, dest_on_device=True)
+            st.run_into_device(p.y[lo:hi], p.N[lo:hi], p.mm[lo:hi] if p.mm is not None else None, opts,
+                               engine.FitBatch(rec.out[: hi - lo], rec.pred[: hi - lo], rec.status[: hi - lo]))
+            torch.cuda.synchronize(dev)  # (the chunks' pinned input staging is reused by the next call)
+    p.release_pinned()
     buf = rec.stage()
     torch.cuda.synchronize(dev)
     parts = gather_records(buf, cap, rank, world)

@@ -14,8 +14,9 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from metadamage_amd.distributed import (NRES_GATHER, REC_BYTES, alloc_records, gather_records, shard_capacity,
-                                        shard_range, unpack_gathered)
+from metadamage_amd.distributed import (FLOAT_COLS, INT_HI, INT_LO, NRES_GATHER, REC_BYTES, alloc_records,
+                                        gather_records, round_like_gather, shard_capacity, shard_range,
+                                        unpack_gathered)
 
 
 def test_shard_ranges_cover_in_order():
@@ -92,9 +93,10 @@ def test_gloo_shard_and_gather_reproduce_single_process(world, T, async_op):
         assert p.exitcode == 0
     b = generate(T, seed=8)
     o, pr, s = OracleLib().fit_batch(b.y, b.N, b.mm, threads=1)
-    # the diagnostic columns stay on the fitting rank: results + reserved only
+    # the diagnostic columns stay on the fitting rank: the 25 result columns
+    # only, the non-count ones rounded to f32 as the frames store them
     assert got[0].shape == (T, NRES_GATHER)
-    np.testing.assert_array_equal(got[0], o[:, :NRES_GATHER])
+    np.testing.assert_array_equal(got[0], round_like_gather(o))
     np.testing.assert_array_equal(got[1], pr)
     np.testing.assert_array_equal(got[2], s)
 
@@ -153,7 +155,7 @@ def test_bench_c4_step_rehearsal(world, total, share):
     assert rows.size == total and (rows == np.arange(total) % share).all()
     b = generate(share, seed=3)
     o, pr, s = OracleLib().fit_batch(b.y[rows], b.N[rows], b.mm[rows], threads=1)
-    np.testing.assert_array_equal(got[0], o[:, :NRES_GATHER])
+    np.testing.assert_array_equal(got[0], round_like_gather(o))
     np.testing.assert_array_equal(got[1], pr)
     np.testing.assert_array_equal(got[2], s)
 
@@ -161,16 +163,29 @@ def test_bench_c4_step_rehearsal(world, total, share):
 @pytest.mark.parametrize("n", [5, 6])
 def test_record_views_layout(n):
     rec = alloc_records(n, "cpu")
-    assert rec.buf.numel() == n * REC_BYTES and REC_BYTES == 564
-    assert rec.out.shape == (n, 80) and rec.res.shape == (n, NRES_GATHER)
+    assert REC_BYTES == 496 and rec.buf.numel() == n * REC_BYTES
+    assert rec.out.shape == (n, 80) and rec.ints.shape == (n, INT_HI - INT_LO)
+    assert rec.floats.shape == (n, len(FLOAT_COLS)) and len(FLOAT_COLS) + INT_HI - INT_LO == NRES_GATHER
     assert rec.pred.shape == (n, 3, 30) and rec.status.shape == (n,)
-    assert rec.res.is_contiguous() and rec.pred.is_contiguous() and rec.status.is_contiguous()
-    assert rec.res.data_ptr() == rec.buf.data_ptr()
-    assert rec.pred.data_ptr() - rec.buf.data_ptr() == n * NRES_GATHER * 8
+    for t in (rec.ints, rec.floats, rec.pred, rec.status):
+        assert t.is_contiguous()
+    assert rec.ints.data_ptr() == rec.buf.data_ptr()
+    assert rec.floats.data_ptr() - rec.buf.data_ptr() == n * 8 * 8
+    assert rec.pred.data_ptr() - rec.floats.data_ptr() == n * 17 * 4
     assert rec.status.data_ptr() - rec.pred.data_ptr() == n * 360
-    rec.out.copy_(torch.arange(n * 80, dtype=torch.float64).view(n, 80))
+    g = torch.Generator().manual_seed(n)
+    rec.out.copy_(torch.rand((n, 80), generator=g, dtype=torch.float64) * 1e3)
+    rec.out[:, INT_LO:INT_HI] = torch.randint(0, 2**32, (n, INT_HI - INT_LO), generator=g).double()
+    rec.out[0, 0] = float("nan")
     rec.stage()
-    np.testing.assert_array_equal(rec.res.numpy(), rec.out[:, :NRES_GATHER].numpy())
+    rec.pred.zero_()
+    rec.status.zero_()
+    got, _, _ = unpack_gathered([rec.buf], n, 1)
+    np.testing.assert_array_equal(got, round_like_gather(rec.out.numpy()))
+    # the counts exact, the rest as the frames' float32 cast rounds them
+    np.testing.assert_array_equal(got[:, INT_LO:INT_HI], rec.out[:, INT_LO:INT_HI].numpy())
+    np.testing.assert_array_equal(got[:, FLOAT_COLS].astype(np.float32),
+                                  rec.out.numpy()[:, FLOAT_COLS].astype(np.float32))
 
 
 def _failing_worker(rank, world, port, q):

@@ -14,7 +14,24 @@ import socket
 import numpy as np
 import pytest
 
+from metadamage_amd.distributed import round_like_gather
+
 pytestmark = pytest.mark.gpu
+
+
+def _frames_equal(p, out, pred, st, ref_out, ref_pred, ref_st):
+    """The written frames of the sharded fit (gathered f32-rounded columns) and
+    of the single-process fit are identical (fits.make_df_fit_*)."""
+    import types
+
+    from metadamage_amd import fits
+
+    cfg = types.SimpleNamespace(shortname="x")
+    a = fits.make_df_fit_results(p, out, st == 0, cfg)
+    b = fits.make_df_fit_results(p, ref_out, ref_st == 0, cfg)
+    assert a.equals(b)
+    assert fits.make_df_fit_predictions(p, pred, st == 0, cfg).equals(
+        fits.make_df_fit_predictions(p, ref_pred, ref_st == 0, cfg))
 
 
 def _free_port():
@@ -76,8 +93,9 @@ def test_sharded_fit_packed_equals_single_process(mode_name):
     ref_out, ref_pred, ref_st = fits.fit_packed(p, opts, shard=False)
     assert out.shape == (T, _lib.NRESULT) and ref_out.shape[0] == T  # (the gather carries the 25 result columns)
     assert np.array_equal(st, ref_st)
-    assert np.array_equal(out[:, :_lib.NRESULT], ref_out[:, :_lib.NRESULT], equal_nan=True)
+    assert np.array_equal(out, round_like_gather(ref_out), equal_nan=True)
     assert np.array_equal(pred, ref_pred, equal_nan=True)
+    _frames_equal(p, out, pred, st, ref_out, ref_pred, ref_st)
 
 
 def _rccl_rank(port, T, q):
@@ -132,5 +150,6 @@ def test_rccl_path_in_a_world_of_one():
     p = fits.Packed(b.tax_id, b.tax_id.astype(str), np.full(T, "species"), b.N_alignments, b.y, b.N, b.mm)
     ref_out, ref_pred, ref_st = fits.fit_packed(p, None, shard=False)
     assert np.array_equal(st, ref_st)
-    assert np.array_equal(out[:, :25], ref_out[:, :25], equal_nan=True)
+    assert np.array_equal(out, round_like_gather(ref_out), equal_nan=True)
     assert np.array_equal(pred, ref_pred, equal_nan=True)
+    _frames_equal(p, out, pred, st, ref_out, ref_pred, ref_st)

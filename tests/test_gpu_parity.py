@@ -140,12 +140,16 @@ def test_hpdi_kernel_vs_scipy_and_oracle(engine, oracle_lib):
     # small end of a window ~1e8 counts wide is a rounding of its ~1e-10 mass
     rel = np.maximum(mixed_rel(lo / N, olo / N), mixed_rel(hi / N, ohi / N))
     assert rel.max() < RTOL, (rel.max(), N[rel.argmax()], D[rel.argmax()], phi[rel.argmax()])
-    # identical counts up to N = 1e6; beyond, the two FP64 evaluations of ln p
-    # (lnGamma differences vs long-double lgamma) may round the window mass
-    # across one count (~1e-8 relative)
+    # identical counts for every window up to N = 1e6 (round 6 on the box: 0 of
+    # the 13,425 differ); beyond, the two FP64 evaluations of ln p (lnGamma
+    # differences vs long-double lgamma) may round the window mass across one
+    # count (~1e-8 relative): 98.7 % of all 20k windows identical
     small = N <= 1e6
-    assert ((lo == olo) & (hi == ohi))[small].mean() > 0.999
-    assert ((lo == olo) & (hi == ohi)).mean() > 0.97
+    same = (lo == olo) & (hi == ohi)
+    print(f"HPDI windows identical: N <= 1e6 {same[small].mean():.6f} ({int((~same[small]).sum())} of "
+          f"{int(small.sum())} differ), all {same.mean():.6f}")
+    assert same[small].all(), np.nonzero(small & ~same)[0][:5]
+    assert same.mean() > 0.98
 
 
 # --------------------------------------------------------------------------

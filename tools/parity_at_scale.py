@@ -29,7 +29,11 @@ def main() -> None:
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", nargs="*", default=None, help="TAXA:SEED pairs (default: C2, C3 size, C4 share)")
-    ap.add_argument("--dump", default=None, help="npz path: the 16 taxa furthest from the oracle, inputs + both records")
+    ap.add_argument("--dump", default=None, help="npz path: the --dump-n taxa furthest from the oracle, inputs + both records")
+    ap.add_argument("--dump-n", type=int, default=64)
+    ap.add_argument("--dump-by", choices=["all", "hpdi"], default="hpdi",
+                    help="rank by every result column, or by the HPDI ones (D_max_{lower,upper}_hpdi and the "
+                    "per-position prediction bounds)")
     a = ap.parse_args()
     sizes = ((10_000, 1, "C2"), (100_000, 2, "C3 size, MAP"), (125_000, 3, "C4 per-GPU share"))
     if a.sizes:
@@ -72,11 +76,17 @@ def main() -> None:
                     oracle_threads=threads)
         print(json.dumps(line), flush=True)
         if a.dump:
-            rel = np.abs(out[:, :25] - ref[:, :25]) / np.maximum(np.abs(ref[:, :25]), 1e-2)
-            rel = np.where(np.isnan(out[:, :25]) & np.isnan(ref[:, :25]), 0.0, rel).max(axis=1)
-            idx = np.argsort(-np.nan_to_num(rel, nan=np.inf))[:16]
-            np.savez(a.dump, idx=idx, rel=rel[idx], y=b.y[idx], N=b.N[idx], mm=b.mm[idx], gpu=out[idx], cpu=ref[idx],
-                     gpu_status=st[idx], cpu_status=rst[idx])
+            cols = [2, 3] if a.dump_by == "hpdi" else list(range(25))
+            rel = np.abs(out[:, cols] - ref[:, cols]) / np.maximum(np.abs(ref[:, cols]), 1e-2)
+            rel = np.where(np.isnan(out[:, cols]) & np.isnan(ref[:, cols]), 0.0, rel).max(axis=1)
+            if a.dump_by == "hpdi":  # the per-position windows too (float32 records)
+                pr = np.abs(pred[:, 1:3].astype(np.float64) - rpred[:, 1:3]) / np.maximum(np.abs(rpred[:, 1:3]), 1e-2)
+                pr = np.where(np.isnan(pred[:, 1:3]) & np.isnan(rpred[:, 1:3]), 0.0, pr).reshape(T, -1).max(axis=1)
+                rel = np.maximum(rel, pr)
+            idx = np.sort(np.argsort(-np.nan_to_num(rel, nan=np.inf))[:a.dump_n])
+            np.savez_compressed(a.dump, idx=idx, rel=rel[idx], seed=seed, n_taxa=T, y=b.y[idx], N=b.N[idx],
+                                mm=b.mm[idx], gpu=out[idx], cpu=ref[idx], cpu_pred=rpred[idx], gpu_pred=pred[idx],
+                                gpu_status=st[idx], cpu_status=rst[idx])
         del b, out, pred, st, ref, rpred, rst
 
 
