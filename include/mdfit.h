@@ -180,6 +180,17 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm,
 int64_t mdfit_workspace_bytes(int64_t n_taxa, const mdfit_opts* opts);
 
 /*
+ * Noise columns of records fitted with mm = NULL (both modes): the three
+ * normalized_noise columns of out[n_taxa][MDFIT_NOUT] from the mismatch counts
+ * mm[n_taxa][30][12] (add_noise_estimates, fits.py:359-376) -- the values a
+ * call with mm writes, bit for bit; taxa with y > N (status 3, NaN record) are
+ * left alone.  Device pointers, stream-ordered.  Lets a host ship the 1,440 B
+ * per taxon of mismatch counts while the fit runs (engine.ChunkedFitter).
+ */
+int mdfit_noise(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t n_taxa, double* out,
+                void* hip_stream);
+
+/*
  * Pointwise beta-binomial log-pmf (numpyro BetaBinomial.log_prob, used by
  * fits.py:59,67 and log_likelihood fits.py:126-133):
  *   out[i] = log C(N,y) + lnB(y+alpha, N-y+beta) - lnB(alpha, beta)

@@ -65,6 +65,7 @@ EXPORTED_SYMBOLS = [
     "mdfit_default_opts",
     "mdfit_fit_batch",
     "mdfit_workspace_bytes",
+    "mdfit_noise",
     "mdfit_betabinom_logpmf",
     "mdfit_special",
     "mdfit_hpdi68",
@@ -134,6 +135,8 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         lib.mdfit_profile_read.argtypes = [vp, vp, vp]
         lib.mdfit_profile_read.restype = ctypes.c_int
     lib.mdfit_workspace_bytes.restype = i64
+    lib.mdfit_noise.argtypes = [vp, vp, vp, i64, vp, vp]
+    lib.mdfit_noise.restype = ctypes.c_int
     lib.mdfit_betabinom_logpmf.argtypes = [vp, vp, vp, vp, i64, vp, vp, vp]
     lib.mdfit_betabinom_logpmf.restype = ctypes.c_int
     lib.mdfit_special.argtypes = [vp, i64, vp, vp]

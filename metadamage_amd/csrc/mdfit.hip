@@ -1074,6 +1074,31 @@ __global__ __launch_bounds__(kWave) void assemble_kernel(
   if (lane == 0) status[t] = st;
 }
 
+// mdfit_noise: the three noise columns (add_noise_estimates, fits.py:359-376)
+// of records fitted with mm = NULL, from the mismatch counts -- the record
+// assembly's own noise code, so the columns are those of a call with mm bit
+// for bit.  One wave per taxon; an invalid taxon (y > N, its record NaN) is
+// left alone.  The host's chunked dispatch ships mm while the fit runs and
+// fills the columns after (engine.ChunkedFitter).
+__global__ __launch_bounds__(kWave) void noise_kernel(const uint32_t* __restrict__ gy,
+                                                      const uint32_t* __restrict__ gN,
+                                                      const uint32_t* __restrict__ gmm, int64_t n_taxa,
+                                                      double* __restrict__ out) {
+  __shared__ uint32_t s_mm[kNPos * kNMM];
+  __shared__ double s_rec[MDFIT_NOUT];
+  __shared__ double s_tmp[kWave];
+  const int lane = threadIdx.x;
+  const int64_t t = blockIdx.x;
+  if (t >= n_taxa) return;
+  const bool bad_lane = lane < kNPos && gy[t * kLD + lane] > gN[t * kLD + lane];
+  if (__any(bad_lane)) return;
+  for (int i = lane; i < kNPos * kNMM; i += kWave) s_mm[i] = gmm[t * (kNPos * kNMM) + i];
+  __syncthreads();
+  record_noise(lane, s_mm, true, s_rec, s_tmp);
+  __syncthreads();
+  if (lane < 3) out[t * MDFIT_NOUT + MDFIT_F_NORMALIZED_NOISE + lane] = s_rec[MDFIT_F_NORMALIZED_NOISE + lane];
+}
+
 // ---------------------------------------------------------------------------
 // K4: 68 % predictive HPDI (MDFIT-HPDI v2, mdfit_hpdi.h) of the PMD-all mode at
 // every position (fits.py:112-120, 260-261).  K4a: one lane per (taxon,
@@ -1900,6 +1925,15 @@ int mdfit_fit_batch(const uint32_t* y, const uint32_t* N, const uint32_t* mm, in
   prof_record(3, s);
   if (g_prof.on && g_prof.n < kProfMax) ++g_prof.n;
   return 0;
+}
+
+int mdfit_noise(const uint32_t* y, const uint32_t* N, const uint32_t* mm, int64_t n_taxa, double* out,
+                void* hip_stream) {
+  if (n_taxa < 0 || (n_taxa > 0 && (!y || !N || !mm || !out))) return set_err(MDFIT_E_ARG, "bad arguments");
+  if (n_taxa == 0) return 0;
+  hipLaunchKernelGGL(mdfit::noise_kernel, dim3((unsigned)n_taxa), dim3(mdfit::kWave), 0, (hipStream_t)hip_stream, y,
+                     N, mm, n_taxa, out);
+  return check_launch("noise_kernel");
 }
 
 int mdfit_betabinom_logpmf(const double* y, const double* N, const double* alpha,

@@ -584,12 +584,8 @@ __device__ __forceinline__ bool newton_dir(bool pmd, const double u[4], const do
 // record pieces shared by the MAP and sampling assembly kernels (one wave per
 // taxon, counts staged in LDS)
 // ---------------------------------------------------------------------------
-// sums (fits.py:272-283) and noise (fits.py:359-376) into the record s_rec;
-// s_tmp: 64 doubles of LDS scratch.  Wave-collective (one 64-lane block).
-__device__ __forceinline__ void record_sums_noise(int lane, const double* s_y, const double* s_N,
-                                                  const uint32_t* s_mm, bool has_mm, double* s_rec,
-                                                  double* s_tmp) {
-  // ---- sums (fits.py:272-283) -------------------------------------------------
+// sums (fits.py:272-283) into the record s_rec.  Wave-collective.
+__device__ __forceinline__ void record_sums(int lane, const double* s_y, const double* s_N, double* s_rec) {
   {
     const double v = lane < kNPos ? 1.0 : 0.0;
     const double fw = lane < kNHalf ? 1.0 : 0.0;
@@ -608,8 +604,13 @@ __device__ __forceinline__ void record_sums_noise(int lane, const double* s_y, c
       s_rec[MDFIT_F_Y_SUM_TOTAL] = yt;
     }
   }
+}
 
-  // ---- noise (fits.py:359-376) -------------------------------------------------
+// noise (fits.py:359-376) of the mismatch counts s_mm[30][12] into the record
+// s_rec (NaN without them); s_tmp: 64 doubles of LDS scratch.  Wave-collective
+// (one 64-lane block).
+__device__ __forceinline__ void record_noise(int lane, const uint32_t* s_mm, bool has_mm, double* s_rec,
+                                             double* s_tmp) {
   {
     // mismatch column j = lane % 12 (AC AG AT CA CG CT GA GC GT TA TC TG), rows
     // i = lane / 12 + 5k (k < 6) on lanes 0..59: 6 rows per lane instead of 30
@@ -677,7 +678,13 @@ __device__ __forceinline__ void record_sums_noise(int lane, const double* s_y, c
       s_rec[MDFIT_F_NORMALIZED_NOISE_REVERSE] = have ? nz[2] : NAN;
     }
   }
+}
 
+__device__ __forceinline__ void record_sums_noise(int lane, const double* s_y, const double* s_N,
+                                                  const uint32_t* s_mm, bool has_mm, double* s_rec,
+                                                  double* s_tmp) {
+  record_sums(lane, s_y, s_N, s_rec);
+  record_noise(lane, s_mm, has_mm, s_rec, s_tmp);
 }
 
 }  // namespace mdfit

@@ -77,6 +77,9 @@ __device__ __forceinline__ Stream make_stream(uint64_t seed, int64_t g, int sub)
   return s;
 }
 
+#ifndef MDFIT_PHILOX_MAD
+#define MDFIT_PHILOX_MAD 0
+#endif
 __device__ __forceinline__ uint4 block(const Stream& s, uint32_t w2, uint32_t w3) {
   uint32_t c0 = s.c0, c1 = s.c1, c2 = w2, c3 = w3, k0 = s.k0, k1 = s.k1;
   // The key is the seed in every stream (make_stream), so it is wave-uniform:
@@ -88,8 +91,14 @@ __device__ __forceinline__ uint4 block(const Stream& s, uint32_t w2, uint32_t w3
   asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
+#if MDFIT_PHILOX_MAD  // one v_mad_u64_u32 per product (hi and lo together)
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+#else
     const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
     const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+#endif
     const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
     c0 = n0;
     c1 = lo1;
@@ -221,6 +230,12 @@ constexpr int kInit = 1, kFind = 2, kIter = 3, kDone = 4;
 #define MDFIT_NUTS_CD_WAVES 4  // 128 VGPRs, no spill with MachineLICM off (build_hip)
 #endif
 
+// the sampler's exponentials: the table exp (fexp_t, ~1 ulp) or the library's
+#ifndef MDFIT_TEXP
+#define MDFIT_TEXP 0
+#endif
+__device__ __forceinline__ double nexp(double x) { return MDFIT_TEXP ? fexp_t(x) : exp(x); }
+
 // ln(1 + e) of the multinomial weights' log-sum-exp, e = exp(-|w1 - w2|) in
 // [0, 1]: the log-weights enter only through exp differences, so absolute
 // accuracy is what counts, and the fast form takes the table log of the
@@ -242,7 +257,7 @@ __device__ __forceinline__ PotC potential_cd(const PointData pt[PPL], double x, 
   constexpr int kG = PPL == 1 ? 16 : 8;
   const int c = (int)(threadIdx.x & 3);
   const bool hi8 = PPL == 2 && (threadIdx.x & 8);
-  const double e = exp(c < 3 ? -fabs(x) : x);
+  const double e = nexp(c < 3 ? -fabs(x) : x);
   // ln(1 + e), e = exp(-|x|) in (0, 1]: it enters only the log prior, whose
   // absolute (not relative) accuracy matters in U ~ 1e5..1e7, so the fast form
   // takes the table log of the rounded 1 + e (absolute error <= 1.2e-16)
@@ -771,7 +786,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       if (isnan(de)) de = INFINITY;
       const double w = -de;
       const int dv = de > kMaxDelta;
-      const double acc = de > 0.0 ? exp(-de) : 1.0;
+      const double acc = de > 0.0 ? nexp(-de) : 1.0;
       if (n_leaf == 0) {
         V[kVsz][c] = zev;
         V[kVsg][c] = P.g;
@@ -782,7 +797,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         C.s_n = 1;
       } else {
         const double m = fmax(s_w, w);
-        const double e = exp(-fabs(s_w - w));
+        const double e = nexp(-fabs(s_w - w));
         const double nw = m == -INFINITY ? -INFINITY : m + lae1p(e);
         const double prob = (w >= s_w ? 1.0 : e) * rcp(1.0 + e);
         if ((leaf_ctr >> 4) != C.ul_chunk) {  // next 16 leaf uniforms, 16 / kG per lane
@@ -854,7 +869,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       if (s_turn || s_div || n_leaf == nmax) {
         NSTAMP(6);
         // merge the subtree into the tree: biased progressive sampling
-        const double em = exp(-fabs(C.t_w - s_w));
+        const double em = nexp(-fabs(C.t_w - s_w));
         const double prob = (s_turn || s_div) ? 0.0 : (s_w > C.t_w ? 1.0 : em);
         if (C.u_tr < prob) {
           V[kVtz][c] = V[kVsz][c];
@@ -897,7 +912,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
             const double wt = 1.0 / (sq * sqrt(sq));  // t^-0.75
             const double x_avg = (1.0 - wt) * C.x_avg + wt * x_t;
             C.x_avg = x_avg;
-            C.eps = exp(it == W - 1 ? x_avg : x_t);
+            C.eps = nexp(it == W - 1 ? x_avg : x_t);
             if (C.eps < kTiny) C.eps = kTiny;
             const int widx = C.widx;
             const int wend = widx < kMaxWin ? swin_end[widx] : -1, nwin = swin_n;
@@ -931,7 +946,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
             const int64_t sidx = ((C.taxon * MDFIT_NSUBFIT + C.sub) * (int64_t)S + (it - W)) * 4;
             if ((!whole || h == 0) && i < 4) {
               const double zj = V[kVtz][c];
-              samples[sidx + i] = i == 3 ? exp(zj) + 2.0 : ((i == 0 || pmd) ? 1.0 / (1.0 + exp(-zj)) : 0.0);
+              samples[sidx + i] = i == 3 ? nexp(zj) + 2.0 : ((i == 0 || pmd) ? 1.0 / (1.0 + nexp(-zj)) : 0.0);
             }
             C.st_div += t_div ? 1.0 : 0.0;
             C.st_leap += (double)nleap;

@@ -72,8 +72,10 @@ __device__ __forceinline__ double flog(double x) {
 #define MDFIT_TLOG_NUTS 1  // the sampler's potential and WAIC: C3 chain + post ~7.0 -> 6.3 s (A/B)
 #endif
 }  // namespace mdfit
+#include "mdfit_exptab.h"
 #include "mdfit_logtab.h"
 namespace mdfit {
+
 // Natural log by table (the lnGamma family's logs: arguments >= 10, and the
 // shift products), ~1 ulp for x away from 1: x = 2^e m, m in [1, 2), j = the
 // top 8 mantissa bits, c_j = 1 + (2j+1)/512 the centre of its interval
@@ -103,7 +105,7 @@ __device__ __forceinline__ double flog_t(double x) {
   const int j = (int)((hw >> 12) & 255u);
   const double m = __hiloint2double((int)((hw & 0x000FFFFFu) | 0x3FF00000u), __double2loint(xn));
   const double2 t = *reinterpret_cast<const double2*>(&g_logtab[j][0]);  // (1/c, ln c)
-  const double c = fma((double)(2 * j + 1), 1.0 / 512.0, 1.0);             // exact
+  const double c = fma((double)(2 * j + 1), 1.0 / 512.0, 1.0);  // exact
   const double r = (m - c) * t.x;
   const double r2 = r * r;
   double q = fma(r, -1.0 / 6.0, 1.0 / 5.0);
@@ -149,6 +151,27 @@ __device__ __forceinline__ double fexp(double x) {
   p = fma(p, r, 1.0);
   const double y = __builtin_amdgcn_ldexp(p, (int)fmax(fmin(n, 1100.0), -1100.0));
   return x < -745.2 ? 0.0 : (x > 709.8 ? INFINITY : y);
+}
+
+// exp(x) by table, ~1 ulp: x = (256 m + j) ln2 / 256 + r, |r| <= ln2 / 512,
+// e^x = 2^m * 2^(j/256) * e^r with 2^(j/256) from mdfit_exptab.h (rounded
+// binary64) and e^r = 1 + r + r^2 (1/2 + r (1/6 + r (1/24 + r / 120)))
+// (truncation < 2^-66).  ln2_hi / 256 times the integer k is exact for |k| <
+// 2^21.  ~20 VALU and one table load against the library exp's ~40.
+// Saturates to 0 / +inf outside [-745.2, 709.78]; NaN passes through.
+__device__ __forceinline__ double fexp_t(double x) {
+#pragma clang fp contract(off)
+  const double k = rint(x * 369.32986822047682);
+  const int ki = (int)fmax(fmin(k, 262144.0), -262144.0);
+  const double r = fma(-k, 1.90821492927058770002e-10 / 256.0,
+                       fma(-k, 6.93147180369123816490e-01 / 256.0, x));
+  double q = fma(r, 1.0 / 120.0, 1.0 / 24.0);
+  q = fma(r, q, 1.0 / 6.0);
+  q = fma(r, q, 0.5);
+  const double p = fma(r * r, q, r);
+  const double t = g_exptab[ki & 255];
+  const double y = __builtin_amdgcn_ldexp(fma(t, p, t), ki >> 8);
+  return x < -745.2 ? 0.0 : (x > 709.78 ? INFINITY : y);
 }
 
 struct LG3 {

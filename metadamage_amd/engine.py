@@ -200,28 +200,43 @@ def default_budget(device) -> int:
 
 
 class _Set:
-    """One chunk's device buffers and the stream its copies and call run on."""
+    """One chunk's device buffers (the workspace is the fitter's: the calls
+    run one after another on the compute stream)."""
 
-    def __init__(self, torch, C: int, device, opts, with_pred: bool, with_mm: bool, dest_on_device: bool):
-        self.stream = torch.cuda.Stream(device=device)
+    def __init__(self, torch, C: int, device, with_pred: bool, with_mm: bool, dest_on_device: bool):
         self.d_y = torch.empty((C, _lib.LD), dtype=torch.int32, device=device)
         self.d_N = torch.empty((C, _lib.LD), dtype=torch.int32, device=device)
         self.d_mm = torch.empty((C, _lib.NPOS, _lib.NMM), dtype=torch.int32, device=device) if with_mm else None
-        self.res = None if dest_on_device else alloc_outputs(C, device=device, with_pred=with_pred, opts=opts)
-        self.ws = self.res.workspace if self.res is not None else alloc_workspace(C, device, opts)
+        self.out = self.pred = self.status = None
+        if not dest_on_device:
+            self.out = torch.empty((C, _lib.NOUT), dtype=torch.float64, device=device)
+            self.pred = (torch.empty((C, _lib.NPRED, _lib.NPOS), dtype=torch.float32, device=device)
+                         if with_pred else None)
+            self.status = torch.empty((C,), dtype=torch.int32, device=device)
+
+
+H_OUT_COLS = _lib.NRESULT  # record columns the host gets back: the 25 result columns
 
 
 class ChunkedFitter:
     """Host-to-device fits of any number of taxa in chunks of at most
-    `chunk_cap` taxa through N_SETS device buffer sets, each on its own stream:
-    chunk k runs H2D -> mdfit_fit_batch -> D2H on set k % N_SETS's stream, so
-    the copies of one chunk overlap the fit of the other and consecutive fits
-    overlap each other's tails.  Device memory is N_SETS x device_bytes(chunk_cap)
-    whatever the batch size (the reference handles any number of taxa in
-    1,000-taxon chunks, fits.py:692-706; one call per file had a capacity cliff:
-    the NUTS draws are 192 KB per taxon, ~1.4M taxa per GPU).
+    `chunk_cap` taxa (the reference handles any number of taxa in 1,000-taxon
+    chunks, fits.py:692-706; one call per file had a capacity cliff: the NUTS
+    draws are 192 KB per taxon, ~1.4M taxa per GPU).  Device memory is
+    N_SETS x device_bytes(chunk_cap) whatever the batch size.
 
-    Outputs go to pinned host buffers (run: the 32 record columns, the
+    Two streams: the caller's current stream runs the calls, one after another
+    (mdfit_fit_batch with mm = NULL, then mdfit_noise once the chunk's mismatch
+    counts are on the device); a copy stream runs every transfer.  So the fit
+    starts as soon as its y, N (256 B per taxon) are in, the mismatch counts
+    (1,440 B per taxon) cross PCIe while it runs, and -- with several chunks --
+    chunk k's results come back while chunk k+1 fits (N_SETS buffer sets).  The
+    transfers of one chunk are ordered y, N before mm so the fit's inputs are
+    not behind the bulk.  (Two streams of ours beside the library's two side
+    streams: four hardware queues, GPU_MAX_HW_QUEUES on the box; more streams
+    would share queues and serialise.)
+
+    Outputs go to pinned host buffers (run: the 25 result columns, the
     predictions, the status; grown as needed and reused) or, run_into_device,
     straight into the caller's device tensors (the sharded fit's gather
     records)."""
@@ -232,8 +247,10 @@ class ChunkedFitter:
         self.chunk_cap = int(chunk_cap)
         self.device = torch.device(device)
         self.with_pred, self.with_mm, self.dest_on_device = with_pred, with_mm, dest_on_device
-        self.sets = [_Set(torch, self.chunk_cap, self.device, opts, with_pred, with_mm, dest_on_device)
+        self.sets = [_Set(torch, self.chunk_cap, self.device, with_pred, with_mm, dest_on_device)
                      for _ in range(N_SETS)]
+        self.ws = alloc_workspace(self.chunk_cap, self.device, opts)
+        self.copy = torch.cuda.Stream(device=self.device)
         self.full_cap = False  # (staging: the chunk capacity is the device budget's, not the batch's)
         self.capacity = 0  # pinned host buffers (input staging for pageable sources, outputs)
         self.h_y = self.h_N = self.h_mm = self.h_out = self.h_pred = self.h_status = None
@@ -247,7 +264,7 @@ class ChunkedFitter:
         self.h_N = torch.empty((cap, _lib.LD), dtype=torch.int32).pin_memory()
         self.h_mm = torch.empty((cap, _lib.NPOS, _lib.NMM), dtype=torch.int32).pin_memory() if self.with_mm else None
         if not self.dest_on_device:
-            self.h_out = torch.empty((cap, 32), dtype=torch.float64).pin_memory()
+            self.h_out = torch.empty((cap, H_OUT_COLS), dtype=torch.float64).pin_memory()
             self.h_pred = (torch.empty((cap, _lib.NPRED, _lib.NPOS), dtype=torch.float32).pin_memory()
                            if self.with_pred else None)
             self.h_status = torch.empty((cap,), dtype=torch.int32).pin_memory()
@@ -269,42 +286,67 @@ class ChunkedFitter:
         return self.h_y[:T], self.h_N[:T], self.h_mm[:T] if use_mm else None
 
     def _launch(self, chunks, src, opts, dest=None):
-        """Enqueue every chunk (asynchronous); returns the sets' streams."""
+        """Enqueue every chunk (asynchronous); returns the event after which
+        every result is in place (host outputs: copied back)."""
         torch = _torch()
+        lib = _lib.load()
         o0 = opts if opts is not None else _lib.default_opts()
         src_y, src_N, src_mm = src
+        comp = torch.cuda.current_stream(self.device)
+        cp = self.copy
+        h_s = _stream_handle(torch, comp)
         start = torch.cuda.Event()
-        start.record(torch.cuda.current_stream(self.device))  # after the caller's prior work
+        start.record(comp)  # after the caller's prior work (and the previous run's)
+        cp.wait_event(start)
+        last_d2h = None
         for k, (lo, hi) in enumerate(chunks):
             st = self.sets[k % N_SETS]
             n = hi - lo
             o = _lib.MdfitOpts.from_buffer_copy(o0)
             o.index_base = o0.index_base + lo  # the sampler's streams: global taxon index
-            st.stream.wait_event(start)
-            with torch.cuda.stream(st.stream):
+            # transfers in: y, N first, then the mismatch counts (copy stream;
+            # the set is free: its previous chunk's D2H came earlier on this stream)
+            with torch.cuda.stream(cp):
                 st.d_y[:n].copy_(src_y[lo:hi], non_blocking=True)
                 st.d_N[:n].copy_(src_N[lo:hi], non_blocking=True)
+                ev_yn = torch.cuda.Event()
+                ev_yn.record(cp)
+                ev_mm = None
                 if src_mm is not None:
                     st.d_mm[:n].copy_(src_mm[lo:hi], non_blocking=True)
-                tm = st.d_mm[:n] if src_mm is not None else None
-                if dest is not None:
-                    res = FitBatch(dest.out[lo:hi], dest.pred[lo:hi] if dest.pred is not None else None,
-                                   dest.status[lo:hi], st.ws)
-                else:
-                    res = FitBatch(st.res.out[:n], st.res.pred[:n] if st.res.pred is not None else None,
-                                   st.res.status[:n], st.ws)
-                fit_batch_device(st.d_y[:n], st.d_N[:n], tm, o, res, stream=st.stream)
-                st.ws = res.workspace
-                if dest is None:
-                    self.h_out[lo:hi].copy_(res.out[:, :32], non_blocking=True)
+                    ev_mm = torch.cuda.Event()
+                    ev_mm.record(cp)
+            if dest is not None:
+                res = FitBatch(dest.out[lo:hi], dest.pred[lo:hi] if dest.pred is not None else None,
+                               dest.status[lo:hi], self.ws)
+            else:
+                res = FitBatch(st.out[:n], st.pred[:n] if st.pred is not None else None, st.status[:n], self.ws)
+            # the call (compute stream) once y, N are in; the noise once mm is
+            comp.wait_event(ev_yn)
+            fit_batch_device(st.d_y[:n], st.d_N[:n], None, o, res, stream=comp)
+            self.ws = res.workspace
+            if ev_mm is not None:
+                comp.wait_event(ev_mm)
+                _lib.check(lib.mdfit_noise(ctypes.c_void_p(st.d_y.data_ptr()), ctypes.c_void_p(st.d_N.data_ptr()),
+                                           ctypes.c_void_p(st.d_mm.data_ptr()), n, ctypes.c_void_p(res.out.data_ptr()),
+                                           h_s))
+            if dest is None:  # results out on the copy stream, behind this chunk's call
+                done = torch.cuda.Event()
+                done.record(comp)
+                cp.wait_event(done)
+                with torch.cuda.stream(cp):
+                    self.h_out[lo:hi].copy_(res.out[:, :H_OUT_COLS], non_blocking=True)
                     if res.pred is not None:
                         self.h_pred[lo:hi].copy_(res.pred, non_blocking=True)
                     self.h_status[lo:hi].copy_(res.status, non_blocking=True)
-        return [st.stream for st in self.sets]
+                last_d2h = cp
+        end = torch.cuda.Event()
+        end.record(cp if last_d2h is not None else comp)
+        return end
 
     def run(self, y, N, mm=None, opts: _lib.MdfitOpts | None = None, sync: bool = True,
             pinned: PinnedPack | None = None, chunks=None):
-        """Fit len(y) taxa; returns numpy views (out[:, :32], pred, status) of the
+        """Fit len(y) taxa; returns numpy views (out[:, :25], pred, status) of the
         pinned buffers (valid until the next run).  pinned: y, N, mm are that
         PinnedPack's views.  chunks: the split (default plan_chunks at this
         staging's chunk_cap)."""
@@ -314,27 +356,20 @@ class ChunkedFitter:
         if chunks and max(hi - lo for lo, hi in chunks) > self.chunk_cap:
             raise ValueError(f"a chunk exceeds this staging's {self.chunk_cap} taxa")
         self._host(T)
-        streams = self._launch(chunks, self._sources(y, N, mm, pinned), opts)
+        end = self._launch(chunks, self._sources(y, N, mm, pinned), opts)
         if sync:
-            for s in streams:
-                s.synchronize()
+            end.synchronize()
         pred = self.h_pred[:T].numpy() if self.h_pred is not None else None
         return self.h_out[:T].numpy(), pred, self.h_status[:T].numpy()
 
     def run_into_device(self, y, N, mm, opts, dest: FitBatch, chunks=None):
         """Fit len(y) taxa chunk by chunk into the caller's device tensors dest
-        (out[T, NOUT], pred, status: rows written in place); stream-ordered
-        before the caller's current stream (which waits for every chunk)."""
-        torch = _torch()
+        (out[T, NOUT], pred, status: rows written in place), ordered on the
+        caller's current stream."""
         T = int(y.shape[0])
         if chunks is None:
             chunks = plan_chunks(T, opts, chunk_taxa=self.chunk_cap)
-        streams = self._launch(chunks, self._sources(y, N, mm, None), opts, dest=dest)
-        cur = torch.cuda.current_stream(self.device)
-        for s in streams:
-            ev = torch.cuda.Event()
-            ev.record(s)
-            cur.wait_event(ev)
+        self._launch(chunks, self._sources(y, N, mm, None), opts, dest=dest)
         return dest
 
 
@@ -439,7 +474,7 @@ def staging(n_taxa: int, device="cuda", opts: _lib.MdfitOpts | None = None, with
 
 def fit_batch_host(y, N, mm=None, opts: _lib.MdfitOpts | None = None, noise=None, device="cuda",
                    pinned: PinnedPack | None = None):
-    """The product's host-to-host fit: (out[T, 32], pred, status), chunked
+    """The product's host-to-host fit: (out[T, 25], pred, status), chunked
     through the device budget (ChunkedFitter).  mm goes to the device (the
     assembly computes the noise columns); without it, `noise` (float64[T][3],
     ingest.noise) fills them when given.  pinned: y, N, mm are views of that

@@ -47,7 +47,8 @@ def test_chunked_host_fit_equals_one_call(torch_dev, monkeypatch, mode, T, chunk
     assert len(engine.plan_chunks(T, opts)) == -(-T // chunk)
     out, pred, st = engine.fit_batch_host(b.y, b.N, b.mm, opts)
     assert np.array_equal(st, ref_st)
-    assert np.array_equal(out[:, :32], ref_out[:, :32], equal_nan=True)
+    assert out.shape[1] == 25
+    assert np.array_equal(out, ref_out[:, :25], equal_nan=True)
     assert np.array_equal(pred, ref_pred, equal_nan=True)
     assert (st == 0).mean() > 0.99
 
