@@ -254,6 +254,7 @@ class ChunkedFitter:
         self.full_cap = False  # (staging: the chunk capacity is the device budget's, not the batch's)
         self.capacity = 0  # pinned host buffers (input staging for pageable sources, outputs)
         self.h_y = self.h_N = self.h_mm = self.h_out = self.h_pred = self.h_status = None
+        self._end = None  # the previous run's last event (its transfers use the pinned buffers)
 
     def _host(self, T: int):
         if T <= self.capacity:
@@ -278,6 +279,8 @@ class ChunkedFitter:
         use_mm = mm is not None and self.with_mm
         if pinned is not None:
             return pinned.h_y[:T], pinned.h_N[:T], pinned.h_mm[:T] if use_mm else None
+        if self._end is not None:  # the previous run's H2D may still read the staging buffers
+            self._end.synchronize()
         self._host(T)
         self.h_y[:T].numpy()[:] = np.asarray(y, dtype=np.uint32).view(np.int32)
         self.h_N[:T].numpy()[:] = np.asarray(N, dtype=np.uint32).view(np.int32)
@@ -299,13 +302,16 @@ class ChunkedFitter:
         start.record(comp)  # after the caller's prior work (and the previous run's)
         cp.wait_event(start)
         last_d2h = None
+        done = []  # per chunk: its call (and noise) finished on the compute stream
         for k, (lo, hi) in enumerate(chunks):
             st = self.sets[k % N_SETS]
             n = hi - lo
             o = _lib.MdfitOpts.from_buffer_copy(o0)
             o.index_base = o0.index_base + lo  # the sampler's streams: global taxon index
-            # transfers in: y, N first, then the mismatch counts (copy stream;
-            # the set is free: its previous chunk's D2H came earlier on this stream)
+            # transfers in: y, N first, then the mismatch counts (copy stream),
+            # once the set's previous chunk has finished reading them
+            if k >= N_SETS:
+                cp.wait_event(done[k - N_SETS])
             with torch.cuda.stream(cp):
                 st.d_y[:n].copy_(src_y[lo:hi], non_blocking=True)
                 st.d_N[:n].copy_(src_N[lo:hi], non_blocking=True)
@@ -330,10 +336,11 @@ class ChunkedFitter:
                 _lib.check(lib.mdfit_noise(ctypes.c_void_p(st.d_y.data_ptr()), ctypes.c_void_p(st.d_N.data_ptr()),
                                            ctypes.c_void_p(st.d_mm.data_ptr()), n, ctypes.c_void_p(res.out.data_ptr()),
                                            h_s))
+            ev_done = torch.cuda.Event()
+            ev_done.record(comp)
+            done.append(ev_done)
             if dest is None:  # results out on the copy stream, behind this chunk's call
-                done = torch.cuda.Event()
-                done.record(comp)
-                cp.wait_event(done)
+                cp.wait_event(ev_done)
                 with torch.cuda.stream(cp):
                     self.h_out[lo:hi].copy_(res.out[:, :H_OUT_COLS], non_blocking=True)
                     if res.pred is not None:
@@ -342,6 +349,7 @@ class ChunkedFitter:
                 last_d2h = cp
         end = torch.cuda.Event()
         end.record(cp if last_d2h is not None else comp)
+        self._end = end
         return end
 
     def run(self, y, N, mm=None, opts: _lib.MdfitOpts | None = None, sync: bool = True,
