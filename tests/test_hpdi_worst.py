@@ -8,8 +8,12 @@ depend on its batch, so these taxa alone reproduce the worst cases of the 1M
 run at every -m gpu run (the reference's columns:
 /root/reference/metadamage/fits.py:112-120, 260-261).
 
-  * CPU: the oracle re-run on the fixture's inputs reproduces its records bit
-    for bit (the fixture is the oracle's, not a stale copy);
+  * CPU: the oracle re-run on the fixture's inputs reproduces its records (the
+    fixture is the oracle's, not a stale copy): bit for bit but for the WAIC
+    difference statistics (n_sigma*, asymmetry: numpy sums of ~1e5-sized
+    terms, whose last bits follow the host CPU's vector width -- <= 1e-11)
+    and the HPDI windows (libm's exp / log pick FMA code paths by CPU: a
+    window end at a near-tie may move one count -- <= 1e-5);
   * GPU: every result column and prediction bound within 2e-5 (mixed
     relative, the columns' 1e-4 bar's floor) of the oracle, statuses equal."""
 
@@ -34,8 +38,13 @@ def fx():
 def test_fixture_is_the_oracles_record(fx, oracle_lib):
     out, pred, st = oracle_lib.fit_batch(fx["y"], fx["N"], fx["mm"], threads=4)
     assert np.array_equal(st, fx["cpu_status"])
-    assert np.array_equal(out[:, :25], fx["cpu"][:, :25], equal_nan=True)
-    assert np.array_equal(pred, fx["cpu_pred"], equal_nan=True)
+    waic, hpdi = [1, 15, 18, 21], [2, 3]
+    plain = [j for j in range(25) if j not in waic + hpdi]
+    assert np.array_equal(out[:, plain], fx["cpu"][:, plain], equal_nan=True)
+    assert mixed_rel(out[:, waic], fx["cpu"][:, waic]).max() <= 1e-11
+    assert mixed_rel(out[:, hpdi], fx["cpu"][:, hpdi]).max() <= 1e-5
+    assert mixed_rel(pred, fx["cpu_pred"]).max() <= 1e-5
+    assert (pred == fx["cpu_pred"]).mean() > 0.99
     assert int(fx["n_taxa"]) == 1_000_000 and int(fx["seed"]) == 3 and len(fx["idx"]) == 64
 
 
