@@ -230,9 +230,31 @@ constexpr int kInit = 1, kFind = 2, kIter = 3, kDone = 4;
 #define MDFIT_NUTS_CD_WAVES 4  // 128 VGPRs, no spill with MachineLICM off (build_hip)
 #endif
 
+// The multinomial weights of an iteration's trajectory (MDFIT_NUTS_LINW):
+// numpyro / the oracle carry the tree's and the subtree's log-weights and
+// combine them by log-sum-exp (an exp and a log per leaf and per merge, and
+// another exp for the acceptance statistic).  Here they are linear, relative
+// to the iteration's largest log-weight so far w_ref (>= 0: the initial
+// point's is 0): a leaf of log-weight w adds exp(w - w_ref), or, when it is
+// the new largest, rescales the tree's and the subtree's sums by
+// exp(w_ref - w) -- one exp per leaf either way, which is also the leaf's
+// acceptance probability min(1, e^w) while w_ref = 0; the progressive
+// sampling probabilities are ratios of the sums (one reciprocal), the merge
+// an add.  Mathematically the oracle's numbers; a decision differs only when
+// a uniform falls within rounding of a probability.
+#ifndef MDFIT_NUTS_LINW
+#define MDFIT_NUTS_LINW 1
+#endif
+// (MDFIT_NUTS_EREF) and the acceptance probability e^w of a leaf below zero
+// after a rescale as its linear weight times exp(w_ref) -- kept as the
+// product of the rescale factors' reciprocals -- instead of a second exp;
+// beyond w_ref = 700 (the product's range) the exp
+#ifndef MDFIT_NUTS_EREF
+#define MDFIT_NUTS_EREF 0
+#endif
 // the sampler's exponentials: the table exp (fexp_t, ~1 ulp) or the library's
 #ifndef MDFIT_TEXP
-#define MDFIT_TEXP 0
+#define MDFIT_TEXP 1
 #endif
 __device__ __forceinline__ double nexp(double x) { return MDFIT_TEXP ? fexp_t(x) : exp(x); }
 
@@ -449,6 +471,8 @@ struct ColdState {
   int sub, attempt, f_call, f_m, f_last, f_dir, t_da, widx, wn, nm_chunk;
   int t_n, t_depth;
   double t_start;  // the wave's trip count when the chain started (MDFIT_NUTS_PRIO)
+  double w_ref;    // (MDFIT_NUTS_LINW) the largest log-weight of the iteration so far
+  double e_ref;    // exp(w_ref), by the product of the rescales (MDFIT_NUTS_EREF)
   double s_acc;    // the subtree's acceptance sum,
   int s_n, ul_chunk;  // size and the chunk of leaf uniforms in sul
 #ifdef MDFIT_DEV_TRIPS  // development: per-chain start / end clock and trips in diag 4, 5, 7
@@ -786,20 +810,51 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       if (isnan(de)) de = INFINITY;
       const double w = -de;
       const int dv = de > kMaxDelta;
+#if MDFIT_NUTS_LINW
+      // s_w: the subtree's weight, C.t_w the tree's, both relative to w_ref
+      double ew, acc;
+      {
+        const double wr = C.w_ref;
+        const double d = w - wr;
+        const double ed = nexp(-fabs(d));  // (w = -inf: 0)
+        if (d > 0.0) {  // the new largest log-weight: rescale the sums
+          C.t_w *= ed;
+          s_w *= ed;
+          C.w_ref = w;
+          if (MDFIT_NUTS_EREF) C.e_ref = C.e_ref * rcp(ed);
+          ew = 1.0;
+          acc = 1.0;  // (w > w_ref >= 0)
+        } else {
+          ew = ed;
+          acc = w >= 0.0 ? 1.0
+                         : (wr == 0.0 ? ed : (MDFIT_NUTS_EREF && wr < 700.0 ? fmin(1.0, ed * C.e_ref) : nexp(w)));
+        }
+      }
+#else
       const double acc = de > 0.0 ? nexp(-de) : 1.0;
+#endif
       if (n_leaf == 0) {
         V[kVsz][c] = zev;
         V[kVsg][c] = P.g;
         C.spe = P.U;
         V[kVss][c] = rn;
+#if MDFIT_NUTS_LINW
+        s_w = ew;
+#else
         s_w = w;
+#endif
         C.s_acc = acc;
         C.s_n = 1;
       } else {
+#if MDFIT_NUTS_LINW
+        const double nw = s_w + ew;
+        const double prob = ew * rcp(nw);  // (nw = 0: NaN, never taken -- the oracle's NaN too)
+#else
         const double m = fmax(s_w, w);
         const double e = nexp(-fabs(s_w - w));
         const double nw = m == -INFINITY ? -INFINITY : m + lae1p(e);
         const double prob = (w >= s_w ? 1.0 : e) * rcp(1.0 + e);
+#endif
         if ((leaf_ctr >> 4) != C.ul_chunk) {  // next 16 leaf uniforms, 16 / kG per lane
 #pragma unroll
           for (int e2 = 0; e2 < 16 / kG; ++e2) {
@@ -869,8 +924,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       if (s_turn || s_div || n_leaf == nmax) {
         NSTAMP(6);
         // merge the subtree into the tree: biased progressive sampling
+#if MDFIT_NUTS_LINW
+        const double prob = (s_turn || s_div) ? 0.0 : (s_w > C.t_w ? 1.0 : s_w * rcp(C.t_w));
+#else
         const double em = nexp(-fabs(C.t_w - s_w));
         const double prob = (s_turn || s_div) ? 0.0 : (s_w > C.t_w ? 1.0 : em);
+#endif
         if (C.u_tr < prob) {
           V[kVtz][c] = V[kVsz][c];
           V[kVtg][c] = V[kVsg][c];
@@ -886,10 +945,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
           V[kVlr][c] = rm;
           V[kVlg][c] = gr;
         }
+#if MDFIT_NUTS_LINW
+        C.t_w = C.t_w + s_w;
+#else
         {
           const double m = fmax(C.t_w, s_w);
           C.t_w = m == -INFINITY ? -INFINITY : m + lae1p(em);
         }
+#endif
         const double trs = V[kVtr][c] + V[kVss][c];
         V[kVtr][c] = trs;
         t_turn = s_turn || (right ? turning_cd<kG>(act, im, olr, rm, trs) : turning_cd<kG>(act, im, rm, olr, trs));
@@ -1025,7 +1088,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       V[kVlg][c] = V[kVrg][c] = gr;
       V[kVtr][c] = rm;
       e0 = C.tpe + kinetic_cd<kG>(act, im, rm);
+#if MDFIT_NUTS_LINW
+      C.t_w = 1.0;  // the initial point's weight exp(0 - w_ref)
+      C.w_ref = 0.0;
+      C.e_ref = 1.0;
+#else
       C.t_w = 0.0;
+#endif
       C.t_acc = 0.0;
       C.t_n = 0;
       C.t_depth = 0;
