@@ -127,6 +127,24 @@ __device__ __noinline__ double normal(const Stream& s, uint32_t w2, uint32_t w3)
   const double u1 = 1.0 - u53(o.x, o.y), u2 = u53(o.z, o.w);
   return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
 }
+// normal k of the Box-Muller pair of one block (k = 0: cos, 1: sin; oracle:
+// nnormal_k) -- the chain's momenta (draw convention 2)
+__device__ __noinline__ double normal_k(const Stream& s, uint32_t w2, uint32_t w3, int k) {
+  const uint4 o = block(s, w2, w3);
+  const double u1 = 1.0 - u53(o.x, o.y), u2 = u53(o.z, o.w);
+  double sn, cs;
+  sincos(6.283185307179586 * u2, &sn, &cs);
+  return sqrt(-2.0 * log(u1)) * (k ? sn : cs);
+}
+// both normals of the pair
+__device__ __noinline__ double2 normal_pair(const Stream& s, uint32_t w2, uint32_t w3) {
+  const uint4 o = block(s, w2, w3);
+  const double u1 = 1.0 - u53(o.x, o.y), u2 = u53(o.z, o.w);
+  double sn, cs;
+  sincos(6.283185307179586 * u2, &sn, &cs);
+  const double r = sqrt(-2.0 * log(u1));
+  return make_double2(r * cs, r * sn);
+}
 // the same, inlined (the post kernel's draws: no call per normal)
 __device__ __forceinline__ double normal_inl(const Stream& s, uint32_t w2, uint32_t w3) {
   const uint4 o = block(s, w2, w3);
@@ -468,7 +486,7 @@ struct ColdState {
   double eps, t_w, t_acc, u_tr;
   double x_avg, g_avg, mu;
   double st_div, st_leap;
-  int sub, attempt, f_call, f_m, f_last, f_dir, t_da, widx, wn, nm_chunk;
+  int sub, attempt, f_call, f_m, f_last, f_dir, t_da, widx, wn, nm_chunk, db_chunk;
   int t_n, t_depth;
   double t_start;  // the wave's trip count when the chain started (MDFIT_NUTS_PRIO)
   double w_ref;    // (MDFIT_NUTS_LINW) the largest log-weight of the iteration so far
@@ -494,8 +512,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   __shared__ ColdState scold[kNSlot];
   __shared__ double sck[8][kWave];                   // checkpoint i of a slot on its lane i: r[4], rsum[4]
   __shared__ double sck8[PPL == 2 ? kNSlot : 1][8];  // PPL 2: checkpoint 8 of a slot
-  __shared__ double sut[16 * kNSlot], sul[16 * kNSlot], snm[16 * kNSlot];
-  __shared__ int sdb[16 * kNSlot];
+  // draw caches per slot (draw convention 2: two draws per Philox block):
+  // sul 32 leaf uniforms, snm the momenta of 8 iterations, sut / sdb the
+  // transition uniforms / direction bits of depths 0-7 of 2 iterations
+  // (entries 0-15) and of depths 8-9 of this one (16-17)
+  __shared__ double sut[18 * kNSlot], sul[32 * kNSlot], snm[32 * kNSlot];
+  __shared__ int sdb[18 * kNSlot];
   __shared__ int swin_end[kMaxWin];
   __shared__ int swin_n;
   // lane layout (re-derived from an opaque lane index at every trip of the
@@ -505,11 +527,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   const int lane = (LANE);                                                                \
   const int r = lane & (kTaskL - 1), h = r / kG, i = r & (kG - 1), row = lane / kG;       \
   const int c = i & 3; /* this lane's vector component */                                 \
-  const int row16 = row * 16;                                                             \
+  const int row18 = row * 18, row32 = row * 32;                                            \
   const int leader = lane & ~(kTaskL - 1);                                                \
   double(*V)[4] = sv[row];                                                                \
   ColdState& C = scold[row];                                                              \
-  (void)h, (void)c, (void)row16, (void)leader, (void)V, (void)C
+  (void)h, (void)c, (void)row18, (void)row32, (void)leader, (void)V, (void)C
   MDFIT_CD_LAYOUT(threadIdx.x);
   // a wave serves its XCD's queue, then the next queues in
   // turn once that one runs dry: the chains are ~1e4 trips long, so the last
@@ -543,7 +565,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
   C.t_w = C.t_acc = C.u_tr = 0.0;
   C.t_n = C.t_depth = 0;
   C.sub = C.attempt = C.f_call = C.f_m = C.f_last = C.f_dir = C.t_da = C.widx = C.wn = 0;
-  C.nm_chunk = -1;
+  C.nm_chunk = C.db_chunk = -1;
   if (lane < kMaxWin) {
     int e, n;
     windows(W, lane, &e, &n);
@@ -674,7 +696,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         pq[p].N = pq[p].valid ? gN[taxon * kLD + colv] : 0u;
       }
       C.st = make_stream(o.seed, o.index_base + taxon, sub);
-      C.nm_chunk = -1;
+      C.nm_chunk = C.db_chunk = -1;
 #ifndef MDFIT_NO_UTIL
       C.t_start = (double)util_trips;
 #endif
@@ -855,15 +877,17 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
         const double nw = m == -INFINITY ? -INFINITY : m + lae1p(e);
         const double prob = (w >= s_w ? 1.0 : e) * rcp(1.0 + e);
 #endif
-        if ((leaf_ctr >> 4) != C.ul_chunk) {  // next 16 leaf uniforms, 16 / kG per lane
+        if ((leaf_ctr >> 5) != C.ul_chunk) {  // next 32 leaf uniforms: 2 per block, 32 / kG per lane
 #pragma unroll
           for (int e2 = 0; e2 < 16 / kG; ++e2) {
             const int ix = i + kG * e2;
-            sul[row16 + ix] = uniform(C.st, (uint32_t)it, 32u + (uint32_t)(leaf_ctr & ~15) + (uint32_t)ix);
+            const uint4 b = block(C.st, (uint32_t)it, 32u + ((uint32_t)(leaf_ctr & ~31) >> 1) + (uint32_t)ix);
+            sul[row32 + 2 * ix] = u53(b.x, b.y);
+            sul[row32 + 2 * ix + 1] = u53(b.z, b.w);
           }
-          C.ul_chunk = leaf_ctr >> 4;
+          C.ul_chunk = leaf_ctr >> 5;
         }
-        if (sul[row16 + (leaf_ctr & 15)] < prob) {
+        if (sul[row32 + (leaf_ctr & 31)] < prob) {
           V[kVsz][c] = zev;
           V[kVsg][c] = P.g;
           C.spe = P.U;
@@ -1032,16 +1056,16 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
           NSTAMP(8);
           // next doubling
           const int j = C.t_depth;
-          if (j == 8) {  // the draws of depths 8 and 9 (entries 8, 9 of the caches)
-            if (i < 4) {
-              const int jj = 8 + (i & 1);
-              const uint4 b = block(C.st, (uint32_t)it, (i < 2 ? 4u : 5u) + 2u * (uint32_t)jj);
-              if (i < 2) sdb[row16 + jj] = (int)(b.x & 1u);
-              else sut[row16 + jj] = u53(b.x, b.y);
+          if (j == 8) {  // the draws of depths 8 and 9 (entries 16, 17 of the caches)
+            if (i < 2) {
+              const uint4 b = block(C.st, (uint32_t)it, 12u + (uint32_t)i);
+              sdb[row18 + 16 + i] = (int)(b.z & 1u);
+              sut[row18 + 16 + i] = u53(b.x, b.y);
             }
           }
-          right = sdb[row16 + j] != 0;
-          C.u_tr = sut[row16 + j];
+          const int e = j < 8 ? 8 * (it & 1) + j : 8 + j;
+          right = sdb[row18 + e] != 0;
+          C.u_tr = sut[row18 + e];
           n_leaf = 0;
           nmax = 1 << j;
           step = right ? C.eps : -C.eps;
@@ -1061,7 +1085,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       }
       mode = kFind;
       C.eps = ldexp(C.eps, C.f_dir);
-      const double nj = normal(C.st, 0xFFFE0000u + 4096u * (uint32_t)C.f_call + (uint32_t)C.f_m, (uint32_t)c);
+      const double nj =
+          normal_k(C.st, 0xFFFE0000u + 4096u * (uint32_t)C.f_call + (uint32_t)C.f_m, (uint32_t)(c >> 1), c & 1);
       rm = act ? nj * V[kVis][c] : 0.0;
       z = V[kVtz][c];
       gr = V[kVtg][c];
@@ -1071,15 +1096,17 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
     if (begin_iter) {
       mode = kIter;
       // this iteration's momenta from the 4-iteration cache
-      if ((it >> 2) != C.nm_chunk) {
+      if ((it >> 3) != C.nm_chunk) {  // the momenta of 8 iterations: lane ix the pair (it, dims 2m, 2m + 1)
 #pragma unroll
         for (int e2 = 0; e2 < 16 / kG; ++e2) {
           const int ix = i + kG * e2;
-          snm[row16 + ix] = normal(C.st, (uint32_t)((it & ~3) + (ix >> 2)), (uint32_t)(ix & 3));
+          const double2 np = normal_pair(C.st, (uint32_t)((it & ~7) + (ix >> 1)), (uint32_t)(ix & 1));
+          snm[row32 + 2 * ix] = np.x;
+          snm[row32 + 2 * ix + 1] = np.y;
         }
-        C.nm_chunk = it >> 2;
+        C.nm_chunk = it >> 3;
       }
-      const double nj = snm[row16 + 4 * (it & 3) + c];
+      const double nj = snm[row32 + 4 * (it & 7) + c];
       rm = act ? nj * V[kVis][c] : 0.0;
       z = V[kVtz][c];
       gr = V[kVtg][c];
@@ -1101,19 +1128,23 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
       t_turn = t_div = 0;
       leaf_ctr = 0;
       nleap = 0;
-      // this iteration's doubling draws for depths 0-7, one Philox block per
-      // entry: entry e < 8 the direction bit of depth e, entry 8 + e its merge
-      // uniform (depths 8-9, reached by a few iterations, at that doubling)
+      // the doubling draws of depths 0-7 of this iteration and the next, one
+      // Philox block per (iteration, depth) -- its direction bit and merge
+      // uniform -- at entry 8 (iteration & 1) + depth (depths 8-9, reached by
+      // a few iterations, at that doubling)
+      if ((it >> 1) != C.db_chunk) {
 #pragma unroll
-      for (int e2 = 0; e2 < 16 / kG; ++e2) {
-        const int ix = i + kG * e2, j = ix & 7;
-        const uint4 b = block(C.st, (uint32_t)it, (ix < 8 ? 4u : 5u) + 2u * (uint32_t)j);
-        if (ix < 8) sdb[row16 + j] = (int)(b.x & 1u);
-        else sut[row16 + j] = u53(b.x, b.y);
+        for (int e2 = 0; e2 < 16 / kG; ++e2) {
+          const int ix = i + kG * e2;
+          const uint4 b = block(C.st, (uint32_t)((it & ~1) + (ix >> 3)), 4u + (uint32_t)(ix & 7));
+          sdb[row18 + ix] = (int)(b.z & 1u);
+          sut[row18 + ix] = u53(b.x, b.y);
+        }
+        C.db_chunk = it >> 1;
       }
       C.ul_chunk = -1;
-      right = sdb[row16] != 0;
-      C.u_tr = sut[row16];
+      right = sdb[row18 + 8 * (it & 1)] != 0;
+      C.u_tr = sut[row18 + 8 * (it & 1)];
       n_leaf = 0;
       nmax = 1;
       step = right ? C.eps : -C.eps;

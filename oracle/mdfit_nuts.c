@@ -44,12 +44,16 @@
  *     fits with the data_forward quirk of :343-348), noise fits.py:359-376
  *
  * Random streams: key = (lo32 seed, hi32 seed); counter = (lo32 g,
- * hi32 g + (sub << 24), word2, word3) with g = index_base + taxon.  Every draw
- * consumes one Philox block: a uniform from words 0-1 (53 bits), a normal by
- * Box-Muller from words 0-1 (radius) and 2-3 (angle).
- *   chain iteration it:   word2 = it; word3 = 0..3 momentum (dim j),
- *                         4 + 2j direction / 5 + 2j transition of doubling j,
- *                         32 + n progressive-sampling uniform of leaf n
+ * hi32 g + (sub << 24), word2, word3) with g = index_base + taxon.  A
+ * uniform takes words 0-1 (53 bits) or 2-3; a pair of normals is Box-Muller
+ * on one block, words 0-1 the radius, 2-3 the angle: cos, then sin (draw
+ * convention 2, round 6: a block yields two draws where the chain kernel
+ * used one -- half the Philox work of its per-iteration draws).
+ *   chain iteration it:   word2 = it; word3 = 0, 1 momentum dims 2m, 2m+1,
+ *                         4 + j doubling j: transition uniform words 0-1,
+ *                         direction bit 0 of word 2,
+ *                         32 + m progressive-sampling uniforms of leaves
+ *                         2m (words 0-1) and 2m + 1 (words 2-3)
  *   init attempt a:       word2 = 0xFFFF0000 + a, word3 = dim
  *   step-size search f,m: word2 = 0xFFFE0000 + 4096 f + m, word3 = dim
  *   predictive draw s, i: word2 = 0xFFFD0000 + s, word3 = (i << 16) + k
@@ -121,6 +125,16 @@ static double nnormal(const nstream* s, uint32_t w2, uint32_t w3) {
   const double u1 = 1.0 - u53(o[0], o[1]); /* (0, 1] */
   const double u2 = u53(o[2], o[3]);
   return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+}
+
+/* the Box-Muller pair of one block: cos (k = 0) or sin (k = 1) */
+static double nnormal_k(const nstream* s, uint32_t w2, uint32_t w3, int k) {
+  uint32_t o[4];
+  nblock(s, w2, w3, o);
+  const double u1 = 1.0 - u53(o[0], o[1]); /* (0, 1] */
+  const double u2 = u53(o[2], o[3]);
+  const double r = sqrt(-2.0 * log(u1)), a = 6.283185307179586 * u2;
+  return r * (k ? sin(a) : cos(a));
 }
 
 /* ---------------------------------------------------------------------------
@@ -264,7 +278,7 @@ typedef struct {
 
 static void momentum(const nctx* cx, const nstream* st, uint32_t w2, const double invm[4], double r[4]) {
   for (int j = 0; j < 4; j++)
-    r[j] = nuts_active(cx->model, j) ? nnormal(st, w2, (uint32_t)j) * sqrt(1.0 / invm[j]) : 0.0;
+    r[j] = nuts_active(cx->model, j) ? nnormal_k(st, w2, (uint32_t)(j >> 1), j & 1) * sqrt(1.0 / invm[j]) : 0.0;
 }
 
 /* numpyro find_reasonable_step_size (hmc_util) */
@@ -327,9 +341,9 @@ static void nuts_step(const nctx* cx, const nstream* st, uint32_t it, double eps
   while (t.depth < NUTS_MAX_DEPTH && !t.turning && !t.diverging) {
     const int j = t.depth;
     uint32_t o[4];
-    nblock(st, it, 4u + 2u * (uint32_t)j, o);
-    const int right = (int)(o[0] & 1u);
-    const double u_tr = nuniform(st, it, 5u + 2u * (uint32_t)j);
+    nblock(st, it, 4u + (uint32_t)j, o);
+    const int right = (int)(o[2] & 1u);
+    const double u_tr = u53(o[0], o[1]);
     /* subtree of 2^depth leaves in the chosen direction */
     ntree s;
     memset(&s, 0, sizeof(s));
@@ -357,7 +371,9 @@ static void nuts_step(const nctx* cx, const nstream* st, uint32_t it, double eps
       } else {
         const double nw = logaddexp(s.weight, w);
         const double prob = exp(w - nw);
-        const double u = nuniform(st, it, 32u + (uint32_t)leaf_ctr);
+        uint32_t ol[4];
+        nblock(st, it, 32u + ((uint32_t)leaf_ctr >> 1), ol);
+        const double u = (leaf_ctr & 1) ? u53(ol[2], ol[3]) : u53(ol[0], ol[1]);
         if (u < prob) {
           memcpy(s.zp, p.z, sizeof(s.zp));
           memcpy(s.gp, p.g, sizeof(s.gp));
