@@ -268,7 +268,7 @@ constexpr int kInit = 1, kFind = 2, kIter = 3, kDone = 4;
 // product of the rescale factors' reciprocals -- instead of a second exp;
 // beyond w_ref = 700 (the product's range) the exp
 #ifndef MDFIT_NUTS_EREF
-#define MDFIT_NUTS_EREF 0
+#define MDFIT_NUTS_EREF 1
 #endif
 // the sampler's exponentials: the table exp (fexp_t, ~1 ulp) or the library's
 #ifndef MDFIT_TEXP

@@ -80,8 +80,12 @@ def test_short_chains_follow_the_oracle_draw_for_draw(nuts_engine, oracle_lib):
     # diagnostics: the adapted step size (exp of the dual-averaging mean, which
     # amplifies the ~1e-9 energy differences) and the leapfrog counts
     np.testing.assert_allclose(out[same, 36::8][:, :6], ro[same, 36::8][:, :6], rtol=1e-6)
-    # (a tree may stop one doubling apart and still pick the same draw)
-    assert np.abs(out[same, 37::8][:, :6] - ro[same, 37::8][:, :6]).max() <= 0.05
+    # (a tree may stop one doubling apart and still pick the same draw: a few
+    # iterations of a few chains, by up to a depth-4 doubling's 16 leaves in
+    # one of the 100 iterations)
+    dl = np.abs(out[same, 37::8][:, :6] - ro[same, 37::8][:, :6])
+    assert dl.max() <= 0.16 + 1e-9, dl.max()
+    assert (dl > 1e-9).mean() <= 0.05, (dl > 1e-9).mean()
 
 
 def _mcse(x, nb=20):
