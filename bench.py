@@ -560,8 +560,7 @@ def host_to_host(engine, b, opts, dev, steps: int, generate=None) -> dict:
             with engine._STAGING_LOCK:
                 st = engine.staging(T, device=dev, opts=opts, with_mm=use_mm)
                 chunks = engine.plan_chunks(T, opts, chunk_taxa=st.chunk_cap)
-                run = lambda: st.run(y, N, mm if use_mm else None, opts, pinned=pp if use_mm else None,  # noqa: E731
-                                     chunks=chunks)
+                run = lambda: st.run(y, N, mm if use_mm else None, opts, pinned=pp, chunks=chunks)  # noqa: E731
                 run()
                 run()
                 ts = []

@@ -487,11 +487,10 @@ def fit_batch_host(y, N, mm=None, opts: _lib.MdfitOpts | None = None, noise=None
     assembly computes the noise columns); without it, `noise` (float64[T][3],
     ingest.noise) fills them when given.  pinned: y, N, mm are views of that
     PinnedPack (copied to the device from there)."""
-    T = int(np.asarray(y).shape[0])
+    T = int(y.shape[0])
     with _STAGING_LOCK:
         st = staging(T, device=device, opts=opts, with_mm=mm is not None)
-        out, pred, status = st.run(y, N, mm, opts, pinned=pinned if mm is not None else None,
-                                   chunks=plan_chunks(T, opts, chunk_taxa=st.chunk_cap))
+        out, pred, status = st.run(y, N, mm, opts, pinned=pinned, chunks=plan_chunks(T, opts, chunk_taxa=st.chunk_cap))
         out, pred, status = out.copy(), pred.copy(), status.copy()
     if mm is None and noise is not None:
         ok = status != _lib.INVALID
