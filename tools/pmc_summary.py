@@ -108,13 +108,16 @@ def sq_decomposition(prof, tag, sq_csv):
 
 def write_summary(prof, tag, name, taxa, bytes_per_taxon, alg_per_taxon, stats_csv, fetch_csv, write_csv, cmd,
                   handoff_override=None):
-    k = f"mdfit::{name}" if name == "fit_kernel" else f"mdfit::nuts::{name}"
+    # (C2's 10k taxa run the one-point-per-lane layout, fit_kernel<1>: the bench's
+    # 125k host-to-host and C4 calls, fit_kernel<2>, are other launches)
+    k = f"mdfit::{name}<1>" if name == "fit_kernel" else f"mdfit::nuts::{name}"
     fetch_kb = counter_mean(fetch_csv, k, "FETCH_SIZE")
     write_kb = counter_mean(write_csv, k, "WRITE_SIZE")
     # kernel names as rocprofv3 prints them: "void mdfit::fit_kernel<1>(...)"
     fk = next((r for r in rows(stats_csv) if k in r["Name"].split("(")[0]), {})
     summary = {
         "kernel": k,
+        "launches": len([1 for r in rows(fetch_csv) if r["Counter_Name"] == "FETCH_SIZE" and k in r["Kernel_Name"]]),
         "taxa_per_launch": taxa,
         "FETCH_SIZE_kB_mean": fetch_kb,
         "WRITE_SIZE_kB_mean": write_kb,
