@@ -270,12 +270,6 @@ constexpr int kInit = 1, kFind = 2, kIter = 3, kDone = 4;
 #ifndef MDFIT_NUTS_EREF
 #define MDFIT_NUTS_EREF 1
 #endif
-// (MDFIT_NUTS_TIER) the potential's lnGamma / psi pairs by the short
-// Stirling series when every lane using a pair has its argument >= 100
-// (mdfit_special.h lg2t)
-#ifndef MDFIT_NUTS_TIER
-#define MDFIT_NUTS_TIER 0
-#endif
 // the sampler's exponentials: the table exp (fexp_t, ~1 ulp) or the library's
 #ifndef MDFIT_TEXP
 #define MDFIT_TEXP 1
@@ -339,14 +333,8 @@ __device__ __forceinline__ PotC potential_cd(const PointData pt[PPL], double x, 
   bool bad_lane = pmd && A + cc >= 1.0;
   double t6l, t6p;
   LG3 t3b;
-  // wave-wide argument tiers (MDFIT_NUTS_TIER, PPL 1): the lanes whose lnGamma
-  // / psi a call's result feeds (running slots' points; the pad lane when its
-  // value is used) all at >= 100 -> the short series (lg2t)
-  const int il = (int)(threadIdx.x & 15);
   if constexpr (PPL == 1) {
-    const bool use3 = run && (pt[0].valid || il == 15);
-    t3b = MDFIT_NUTS_TIER ? lg2t(pt[0].N + phi, __all(!use3 || pt[0].N + phi >= 100.0))
-                          : lg3<false, MDFIT_TLOG_NUTS>(pt[0].N + phi);
+    t3b = lg3<false, MDFIT_TLOG_NUTS>(pt[0].N + phi);
     t6l = rowb<15>(t3b.l);  // pad lane: lg(0 + phi)
     t6p = rowb<15>(t3b.p);
   } else {
@@ -371,15 +359,8 @@ __device__ __forceinline__ PotC potential_cd(const PointData pt[PPL], double x, 
     }
     bad_lane = bad_lane || (pd.valid && !(D < 1.0));
     const double a = D * phi, b = (1.0 - D) * phi;
-    LG3 t1, t2;
-    if (PPL == 1 && MDFIT_NUTS_TIER) {
-      const bool use12 = run && (pd.valid || (null_wave && il == 15));
-      t1 = lg2t(pd.y + a, __all(!use12 || pd.y + a >= 100.0));
-      t2 = lg2t(pd.N - pd.y + b, __all(!use12 || pd.N - pd.y + b >= 100.0));
-    } else {
-      t1 = lg3<false, MDFIT_TLOG_NUTS>(pd.y + a);
-      t2 = lg3<false, MDFIT_TLOG_NUTS>(pd.N - pd.y + b);
-    }
+    const LG3 t1 = lg3<false, MDFIT_TLOG_NUTS>(pd.y + a);
+    const LG3 t2 = lg3<false, MDFIT_TLOG_NUTS>(pd.N - pd.y + b);
     LG3 t4, t5;
     if (PPL == 1 && null_wave) {
       // every chain of the wave samples model_null: a = q phi is the row's, and
@@ -393,19 +374,13 @@ __device__ __forceinline__ PotC potential_cd(const PointData pt[PPL], double x, 
       // hold the same |z| lane by lane, so a lane and its partner 16 away share
       // a, b -- the even row takes lg3(a), the odd row lg3(b), exchanged (xrow)
       const bool odd = (threadIdx.x & 16) != 0;
-      const double xm = odd ? b : a;
-      const LG3 mine = MDFIT_NUTS_TIER ? lg2t(xm, __all(!(run && pd.valid) || xm >= 100.0))
-                                       : lg3<false, MDFIT_TLOG_NUTS>(xm);
+      const LG3 mine = lg3<false, MDFIT_TLOG_NUTS>(odd ? b : a);
       LG3 other;
       other.l = xrow(mine.l);
       other.p = xrow(mine.p);
       other.q = 0.0;
       t4 = odd ? other : mine;
       t5 = odd ? mine : other;
-    } else if (PPL == 1 && MDFIT_NUTS_TIER) {
-      const bool use45 = run && pd.valid;
-      t4 = lg2t(a, __all(!use45 || a >= 100.0));
-      t5 = lg2t(b, __all(!use45 || b >= 100.0));
     } else {
       t4 = lg3<false, MDFIT_TLOG_NUTS>(a);
       t5 = lg3<false, MDFIT_TLOG_NUTS>(b);

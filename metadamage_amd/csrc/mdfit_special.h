@@ -244,27 +244,6 @@ __device__ __forceinline__ LG3 lg3(double x) {
   return {L, Ps, Q};
 }
 
-// lg3's fast form (no trigamma) with the argument's range known wave-wide:
-// big = every lane that uses the result has x >= 100, where the Stirling
-// series need three terms each (the first omitted terms, 1/(1680 x^7) of
-// lnGamma and 1/(240 x^8) of psi, are < 6e-18 absolute at x = 100: far below
-// an ulp of lnGamma(100) = 359 or psi(100) = 4.6) -- 4 FMAs and their
-// constants instead of 12.  big must be wave-uniform (an __all of the
-// callers' predicate): the branch then costs no divergence.
-__device__ __forceinline__ LG3 lg2t(double x, bool big) {
-#pragma clang fp contract(off)
-  if (!big) return lg3<false, true>(x);
-  constexpr double kHalfLog2Pi = 0.91893853320467274178;
-  const double r = rcp1(x);
-  const double r2 = r * r;
-  const double lx = flog_t(x);
-  double sl = fma(r2, -1.0 / 1260.0, 1.0 / 360.0);
-  sl = fma(r2, -sl, 1.0 / 12.0);
-  double sp = fma(r2, -1.0 / 252.0, 1.0 / 120.0);
-  sp = fma(r2, -sp, 1.0 / 12.0);
-  return {fma(r, sl, fma(x - 0.5, lx, -x) + kHalfLog2Pi), fma(-r2, sp, fma(-0.5, r, lx)), 0.0};
-}
-
 // lnGamma alone (the unused psi is dead code after inlining)
 __device__ __forceinline__ double lgam(double x) { return lg3<false>(x).l; }
 
