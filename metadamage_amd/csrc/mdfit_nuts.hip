@@ -145,11 +145,25 @@ __device__ __noinline__ double2 normal_pair(const Stream& s, uint32_t w2, uint32
   const double r = sqrt(-2.0 * log(u1));
   return make_double2(r * cs, r * sn);
 }
+// (MDFIT_POST_FAST) the post kernel's transcendentals by the table forms:
+// the WAIC's log-sum-exp exponentials and the predictive draws' exponentials
+// and logs (positive normal arguments; absolute accuracy ~1e-16 near 1, which
+// is what their comparisons and the draws need) -- fexp_t / flog_t for the
+// library's exp / log
+#ifndef MDFIT_POST_FAST
+#define MDFIT_POST_FAST 1
+#endif
+#ifndef MDFIT_NUTS_SST
+#define MDFIT_NUTS_SST 1
+#endif
+__device__ __forceinline__ double pexp(double x) { return MDFIT_POST_FAST ? fexp_t(x) : exp(x); }
+__device__ __forceinline__ double plog(double x) { return MDFIT_POST_FAST ? flog_t<true>(x) : log(x); }
+
 // the same, inlined (the post kernel's draws: no call per normal)
 __device__ __forceinline__ double normal_inl(const Stream& s, uint32_t w2, uint32_t w3) {
   const uint4 o = block(s, w2, w3);
   const double u1 = 1.0 - u53(o.x, o.y), u2 = u53(o.z, o.w);
-  return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+  return sqrt(-2.0 * plog(u1)) * cos(6.283185307179586 * u2);
 }
 
 __device__ __forceinline__ bool active(bool pmd, int j) { return pmd || j == 0 || j == 3; }
@@ -275,6 +289,7 @@ constexpr int kInit = 1, kFind = 2, kIter = 3, kDone = 4;
 #define MDFIT_TEXP 1
 #endif
 __device__ __forceinline__ double nexp(double x) { return MDFIT_TEXP ? fexp_t(x) : exp(x); }
+
 
 // ln(1 + e) of the multinomial weights' log-sum-exp, e = exp(-|w1 - w2|) in
 // [0, 1]: the log-weights enter only through exp differences, so absolute
@@ -1033,7 +1048,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
             const int64_t sidx = ((C.taxon * MDFIT_NSUBFIT + C.sub) * (int64_t)S + (it - W)) * 4;
             if ((!whole || h == 0) && i < 4) {
               const double zj = V[kVtz][c];
+#if MDFIT_NUTS_SST  // one exponential per lane: exp(z3) + 2 on lane 3, the sigmoid on lanes 0-2
+              const double ez = nexp(i == 3 ? zj : -zj);
+              samples[sidx + i] = i == 3 ? ez + 2.0 : ((i == 0 || pmd) ? rcp(1.0 + ez) : 0.0);
+#else
               samples[sidx + i] = i == 3 ? nexp(zj) + 2.0 : ((i == 0 || pmd) ? 1.0 / (1.0 + nexp(-zj)) : 0.0);
+#endif
             }
             C.st_div += t_div ? 1.0 : 0.0;
             C.st_leap += (double)nleap;
@@ -1180,7 +1200,7 @@ struct Draw {
 __device__ double log_gamma_draw(Draw& d, double alpha) {
   double boost = 0.0;
   if (alpha < 1.0) {
-    boost = log(1.0 - d.uni()) / alpha;
+    boost = plog(1.0 - d.uni()) / alpha;
     alpha += 1.0;
   }
   const double dd = alpha - 1.0 / 3.0, cc = 1.0 / sqrt(9.0 * dd);
@@ -1190,10 +1210,10 @@ __device__ double log_gamma_draw(Draw& d, double alpha) {
     if (v <= 0.0) continue;
     v = v * v * v;
     const double u = d.uni();
-    if (u < 1.0 - 0.0331 * x * x * x * x) return log(dd * v) + boost;
-    if (log(u) < 0.5 * x * x + dd * (1.0 - v + log(v))) return log(dd * v) + boost;
+    if (u < 1.0 - 0.0331 * x * x * x * x) return plog(dd * v) + boost;
+    if (plog(u) < 0.5 * x * x + dd * (1.0 - v + plog(v))) return plog(dd * v) + boost;
   }
-  return log(dd) + boost;
+  return plog(dd) + boost;
 }
 
 __device__ double binomial_draw(Draw& d, double n, double p) {
@@ -1204,7 +1224,7 @@ __device__ double binomial_draw(Draw& d, double n, double p) {
   double k;
   if (n * pp < 10.0) {
     const double u = d.uni();
-    double pmf = exp(n * log1p(-pp)), cdf = pmf;
+    double pmf = pexp(n * log1p(-pp)), cdf = pmf;
     k = 0.0;
     const double ratio = pp / qq;
     while (u > cdf && k < n && k < 10000.0) {
@@ -1216,7 +1236,7 @@ __device__ double binomial_draw(Draw& d, double n, double p) {
     const double spq = sqrt(n * pp * qq), bb = 1.15 + 2.53 * spq;
     const double aa = -0.0873 + 0.0248 * bb + 0.01 * pp, cc = n * pp + 0.5;
     const double vr = 0.92 - 4.2 / bb, alpha = (2.83 + 5.1 / bb) * spq;
-    const double lpq = log(pp / qq), m = floor((n + 1.0) * pp);
+    const double lpq = plog(pp / qq), m = floor((n + 1.0) * pp);
     const double hh = lg3<false>(m + 1.0).l + lg3<false>(n - m + 1.0).l;
     k = floor(cc);
     for (int it = 0; it < 256; ++it) {
@@ -1228,7 +1248,7 @@ __device__ double binomial_draw(Draw& d, double n, double p) {
         k = kk;
         break;
       }
-      const double lv = log(v * alpha / (aa / (us * us) + bb));
+      const double lv = plog(v * alpha / (aa / (us * us) + bb));
       if (lv <= hh - lg3<false>(kk + 1.0).l - lg3<false>(n - kk + 1.0).l + (kk - m) * lpq) {
         k = kk;
         break;
@@ -1251,7 +1271,7 @@ __device__ int64_t predictive_count(const Stream& st, int s, int col, int k, dou
   const double D = d_at(th, true, k);
   Draw d{&st, 0xFFFD0000u + (uint32_t)s, (uint32_t)col << 16};
   const double lx = log_gamma_draw(d, D * th[3]), ly = log_gamma_draw(d, (1.0 - D) * th[3]);
-  const double p = 1.0 / (1.0 + exp(ly - lx));
+  const double p = 1.0 / (1.0 + pexp(ly - lx));
   const double obs = binomial_draw(d, Nn, p);
   return (obs >= 0.0 && obs <= Nn) ? (int64_t)obs : -1;
 }
@@ -1398,10 +1418,10 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
           // exp(lp - mx) = 0 for every mx: nothing to add (and with mxl still
           // -inf the else branch would form exp(-inf + inf) = NaN)
         } else if (lp > mxl) {
-          sel = sel * exp(mxl - lp) + 1.0;
+          sel = sel * pexp(mxl - lp) + 1.0;
           mxl = lp;
         } else {
-          sel += exp(lp - mxl);
+          sel += pexp(lp - mxl);
         }
         cnt += 1.0;
         const double dlt = lp - mul;
@@ -1409,7 +1429,7 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
         m2l = fma(dlt, lp - mul, m2l);
       }
       const double mx = wmax(mxl);
-      const double se = wsum(cnt > 0.0 ? sel * exp(mxl - mx) : 0.0);
+      const double se = wsum(cnt > 0.0 ? sel * pexp(mxl - mx) : 0.0);
       const double mean = wsum(cnt * mul) / S;
       const double dm = mul - mean;
       const double var = wsum(m2l + cnt * dm * dm) / S;
