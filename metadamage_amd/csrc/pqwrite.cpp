@@ -12,10 +12,16 @@
 // chunks of a row group are encoded on Arrow's CPU pool in parallel.  The file
 // reads back identical with any pyarrow (tests/test_counts.py).
 //
+// Round 6: the page compression (snappy or none) and the columns that carry
+// statistics are parameters: the streamed pipeline writes its large tables
+// (the counts cache, the per-position predictions) uncompressed with
+// statistics on tax_id only -- half the encoding CPU of snappy pages on the
+// count columns, which compress ~2x at best.
+//
 // C ABI (ctypes):
 //   mdpq_unwrap(PyObject* table) -> handle   (call with the GIL held: PyDLL)
-//   mdpq_write(handle, path, dict_cols, n_dict, row_group_rows) -> 0 / -1
-//                                          (GIL released: CDLL; frees handle)
+//   mdpq_write(handle, path, dict_cols, n_dict, stat_cols, n_stat, snappy,
+//              row_group_rows) -> 0 / -1     (GIL released: CDLL; frees handle)
 //   mdpq_free(handle), mdpq_last_error()
 #include <Python.h>
 
@@ -60,7 +66,8 @@ void* mdpq_unwrap(PyObject* obj) {
 
 void mdpq_free(void* h) { delete static_cast<Handle*>(h); }
 
-int mdpq_write(void* h, const char* path, const char** dict_cols, int n_dict, int64_t row_group_rows) {
+int mdpq_write(void* h, const char* path, const char** dict_cols, int n_dict, const char** stat_cols, int n_stat,
+               int snappy, int64_t row_group_rows) {
   std::unique_ptr<Handle> hd(static_cast<Handle*>(h));
   if (!hd || !hd->table || !path) {
     g_err = "bad arguments";
@@ -68,13 +75,11 @@ int mdpq_write(void* h, const char* path, const char** dict_cols, int n_dict, in
   }
   parquet::WriterProperties::Builder wb;
   wb.version(parquet::ParquetVersion::PARQUET_2_6);
-  wb.compression(parquet::Compression::SNAPPY);
+  wb.compression(snappy ? parquet::Compression::SNAPPY : parquet::Compression::UNCOMPRESSED);
   wb.disable_dictionary();
   wb.disable_statistics();
-  for (int i = 0; i < n_dict; ++i) {
-    wb.enable_dictionary(dict_cols[i]);
-    wb.enable_statistics(dict_cols[i]);
-  }
+  for (int i = 0; i < n_dict; ++i) wb.enable_dictionary(dict_cols[i]);
+  for (int i = 0; i < n_stat; ++i) wb.enable_statistics(stat_cols[i]);
   parquet::ArrowWriterProperties::Builder ab;
   ab.set_use_threads(true);
   ab.store_schema();

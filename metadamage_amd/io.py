@@ -42,7 +42,7 @@ def _native_writer():
             py.mdpq_unwrap.argtypes = [ctypes.py_object]
             py.mdpq_unwrap.restype = ctypes.c_void_p
             c.mdpq_write.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
-                                     ctypes.c_int64]
+                                     ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.c_int, ctypes.c_int64]
             c.mdpq_write.restype = ctypes.c_int
             c.mdpq_last_error.restype = ctypes.c_char_p
             py.mdpq_last_error.restype = ctypes.c_char_p
@@ -50,21 +50,35 @@ def _native_writer():
     return _PQ or None
 
 
-def write_table(table: "pa.Table", path, dict_cols) -> None:
+def write_table(table: "pa.Table", path, dict_cols, stat_cols=None, compression: str = "snappy") -> None:
     """pq.write_table(table, path, version="2.6", use_dictionary=dict_cols,
-    write_statistics=dict_cols) -- natively when libmdpq.so is built."""
+    write_statistics=stat_cols (default: dict_cols), compression=compression)
+    -- natively when libmdpq.so is built."""
+    if compression not in ("snappy", "none"):
+        raise ValueError(f"compression must be 'snappy' or 'none', got {compression!r}")
+    stat_cols = list(dict_cols) if stat_cols is None else list(stat_cols)
     nat = _native_writer()
     if nat is None:
         pq.write_table(table, path, version=PARQUET_VERSION, use_dictionary=list(dict_cols) or False,
-                       write_statistics=list(dict_cols) or False)
+                       write_statistics=stat_cols or False, compression=compression)
         return
     py, c = nat
     h = py.mdpq_unwrap(table)
     if not h:
         raise RuntimeError(f"mdpq_unwrap: {py.mdpq_last_error().decode()}")
     names = (ctypes.c_char_p * max(1, len(dict_cols)))(*[n.encode() for n in dict_cols])
-    if c.mdpq_write(h, os.fsencode(str(path)), names, len(dict_cols), 0) != 0:
+    stats = (ctypes.c_char_p * max(1, len(stat_cols)))(*[n.encode() for n in stat_cols])
+    if c.mdpq_write(h, os.fsencode(str(path)), names, len(dict_cols), stats, len(stat_cols),
+                    int(compression == "snappy"), 0) != 0:
         raise OSError(f"{path}: {c.mdpq_last_error().decode()}")
+
+
+# tables of at least this many rows (the counts cache, the per-position
+# predictions: 30 rows per taxon) are written uncompressed with statistics on
+# tax_id only (the key io.Parquet.load filters on): their count / float columns
+# compress ~2x at best under snappy, which costs half the encoding CPU of the
+# host-bound multi-file pipeline (DESIGN.md §10)
+PLAIN_MIN_ROWS = 1_000_000
 
 
 class Parquet:
@@ -108,17 +122,22 @@ class Parquet:
         """Same schema and metadata as the reference's save; the encoding keeps
         dictionaries and column statistics to the categorical columns (the ones
         readers filter on), which writes a counts table ~1.6x faster than
-        dictionary-encoding every numeric column too.  Plain + snappy pages
-        read back with any pyarrow, including the reference's ^2.0 pin."""
+        dictionary-encoding every numeric column too; tables of PLAIN_MIN_ROWS
+        rows and more go uncompressed with statistics on tax_id only.  Plain
+        pages (snappy or none) read back with any pyarrow, including the
+        reference's ^2.0 pin."""
         utils.init_parent_folder(self.filename)
         table = self._add_metadata_to_table(pa.Table.from_pandas(df), metadata)
         cats = [f.name for f in table.schema if pa.types.is_dictionary(f.type)]
+        big = table.num_rows >= PLAIN_MIN_ROWS
+        stats = ([c for c in cats if c == "tax_id"] if big else cats)
+        comp = "none" if big else "snappy"
         # written next to the target and renamed into place: a reader (another
         # rank's cache check, a writer thread of the next file) sees either no
         # file or a complete one, never a half-written parquet
         tmp = self.filename.with_name(f".{self.filename.name}.{os.getpid()}.{threading.get_ident()}.tmp")
         try:
-            write_table(table, tmp, cats)
+            write_table(table, tmp, cats, stats, comp)
             os.replace(tmp, self.filename)
         finally:
             if tmp.exists():

@@ -29,15 +29,17 @@ def _frame(n):
 
 
 @pytest.mark.skipif(io._native_writer() is None, reason="libmdpq.so not built")
-@pytest.mark.parametrize("n", [0, 1, 1000, 1_300_000])
-def test_native_writer_matches_write_table(tmp_path, n):
+@pytest.mark.parametrize("n,comp", [(0, "snappy"), (1, "snappy"), (1000, "snappy"), (1_300_000, "snappy"),
+                                    (1000, "none"), (1_300_000, "none")])
+def test_native_writer_matches_write_table(tmp_path, n, comp):
     df = _frame(n)
     meta = {"out_dir": "x", "N_fits": 3}
     table = io.Parquet(tmp_path / "a")._add_metadata_to_table(pa.Table.from_pandas(df), meta)
     cats = [f.name for f in table.schema if pa.types.is_dictionary(f.type)]
-    io.write_table(table, tmp_path / "native.parquet", cats)
+    stats = cats if comp == "snappy" else ["tax_id"]
+    io.write_table(table, tmp_path / "native.parquet", cats, stats, comp)
     pq.write_table(table, tmp_path / "pyarrow.parquet", version="2.6", use_dictionary=cats or False,
-                   write_statistics=cats or False)
+                   write_statistics=stats or False, compression=comp)
     a, b = pq.read_table(tmp_path / "native.parquet"), pq.read_table(tmp_path / "pyarrow.parquet")
     assert a.equals(b) and a.schema.equals(b.schema, check_metadata=True)
     ma, mb = pq.ParquetFile(tmp_path / "native.parquet").metadata, pq.ParquetFile(tmp_path / "pyarrow.parquet").metadata
@@ -49,9 +51,14 @@ def test_native_writer_matches_write_table(tmp_path, n):
             ca, cb = ma.row_group(i).column(j), mb.row_group(i).column(j)
             assert set(ca.encodings) == set(cb.encodings), (ca.path_in_schema, ca.encodings, cb.encodings)
             assert (ca.statistics is None) == (cb.statistics is None), ca.path_in_schema
-            assert ca.compression == cb.compression == "SNAPPY"
-    # the reference's reader path (io.Parquet.load) gives the same frame
+            assert ca.compression == cb.compression == ("SNAPPY" if comp == "snappy" else "UNCOMPRESSED")
+    # the reference's reader path (io.Parquet.load) gives the same frame (save:
+    # uncompressed from io.PLAIN_MIN_ROWS rows)
     io.Parquet(tmp_path / "c.parquet").save(df, metadata=meta)
+    big = n >= io.PLAIN_MIN_ROWS
+    mc = pq.ParquetFile(tmp_path / "c.parquet").metadata
+    if mc.num_row_groups:
+        assert mc.row_group(0).column(0).compression == ("UNCOMPRESSED" if big else "SNAPPY")
     back = io.Parquet(tmp_path / "c.parquet").load()
     assert back.equals(io.Parquet(tmp_path / "pyarrow.parquet").load())
     assert io.Parquet(tmp_path / "c.parquet").load_metadata() == meta
