@@ -26,6 +26,15 @@ extern "C" {
 #define MDI_E_PARSE (-2)  /* malformed row (message names line and column) */
 #define MDI_E_ARG (-3)
 #define MDI_E_RANGE (-4)  /* a kept count above uint32 (utils.py:338-339 "too large values") */
+#define MDI_E_LAYOUT (-5) /* mdi_used_codes: the distinct categories among codes[n] (pd.unique of a
+ * categorical column, utils.py:121-130; the present groups of fits.py:736-744):
+ * used[k] = 1 where code k (< n_cat) occurs, *n_missing (nullable) = the codes
+ * < 0 (missing values); returns the number of used codes, MDI_E_ARG on a code
+ * >= n_cat.  Parallel over row ranges. */
+int64_t mdi_used_codes(int64_t n, const int32_t* codes, int32_t n_cat, int n_threads, uint8_t* used,
+                       int64_t* n_missing);
+
+/* mdi_pack_dense: the table is not in the usual layout */
 
 /* string columns, interned: codes index the table's string list (first
  * appearance order) */
@@ -123,6 +132,17 @@ int mdi_remap(int64_t n, int n_cols, int32_t* const* codes, const int32_t* const
  * columns: the [T][30][12] mismatch block), parallel over row ranges. */
 int64_t mdi_first_index(int64_t n, const int32_t* codes, int32_t n_cat, int64_t* taxon, int64_t* first);
 int mdi_interleave(int64_t n, int n_cols, const uint32_t* const* cols, uint32_t* out, int n_threads);
+
+/* mdi_pack_dense: fits.pack_counts in one parallel pass for the usual table --
+ * n = 30 T rows, taxon t on rows 30t..30t+29 with positions 1..15, -1..-15 and
+ * one tax_id code (< n_cat) per block, no code in two blocks.  cols: 16 uint32
+ * columns, the 12 mismatch columns (fits.MM_COLUMNS order) then y forward,
+ * y reverse, N forward, N reverse.  Writes y, N (uint32[T][ld], columns >= 30
+ * zeroed) and mm (uint32[T][30][12]); returns T, MDI_E_LAYOUT when the table
+ * is not in that layout (the outputs are then partly written: the caller's general path
+ * rewrites them), MDI_E_ARG on bad arguments. */
+int64_t mdi_pack_dense(int64_t n, const int32_t* codes, int32_t n_cat, const int8_t* position,
+                       const uint32_t* const* cols, int ld, int n_threads, uint32_t* y, uint32_t* N, uint32_t* mm);
 
 /* Worker threads the library uses when a call passes n_threads <= 0: the
  * process's CPU share -- OMP_NUM_THREADS when set (a GPU box grants 16 cores

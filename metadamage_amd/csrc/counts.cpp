@@ -400,6 +400,100 @@ int mdi_interleave(int64_t n, int n_cols, const uint32_t* const* cols, uint32_t*
   return 0;
 }
 
+int64_t mdi_used_codes(int64_t n, const int32_t* codes, int32_t n_cat, int n_threads, uint8_t* used,
+                       int64_t* n_missing) {
+  if (n < 0 || n_cat < 0 || (n > 0 && !codes) || (n_cat > 0 && !used)) return arg_error("mdi_used_codes: bad arguments");
+  const int nt = pool_size(n_threads, n);
+  std::vector<std::vector<uint8_t>> seen((size_t)nt);
+  std::vector<int64_t> miss((size_t)nt, 0);
+  std::vector<uint8_t> bad((size_t)nt, 0);
+  for_ranges(nt, n, [&](int tid, int64_t lo, int64_t hi) {
+    std::vector<uint8_t>& u = seen[(size_t)tid];
+    u.assign((size_t)n_cat, 0);
+    int64_t m = 0;
+    bool b = false;
+    for (int64_t i = lo; i < hi; ++i) {
+      const int32_t k = codes[i];
+      if (k < 0) {
+        ++m;
+      } else if (k >= n_cat) {
+        b = true;
+      } else {
+        u[(size_t)k] = 1;
+      }
+    }
+    miss[(size_t)tid] = m;
+    bad[(size_t)tid] = b;
+  });
+  int64_t m = 0;
+  for (int i = 0; i < nt; ++i) {
+    if (bad[(size_t)i]) return arg_error("mdi_used_codes: code out of its table");
+    m += miss[(size_t)i];
+  }
+  if (n_missing) *n_missing = m;
+  std::vector<int64_t> cnt((size_t)nt, 0);
+  for_ranges(pool_size(n_threads, n_cat), n_cat, [&](int tid, int64_t lo, int64_t hi) {
+    int64_t c = 0;
+    for (int64_t k = lo; k < hi; ++k) {
+      uint8_t v = 0;
+      for (int i = 0; i < nt; ++i) v |= seen[(size_t)i][(size_t)k];
+      used[k] = v;
+      c += v;
+    }
+    cnt[(size_t)tid] = c;
+  });
+  int64_t k = 0;
+  for (int64_t c : cnt) k += c;
+  return k;
+}
+
+int64_t mdi_pack_dense(int64_t n, const int32_t* codes, int32_t n_cat, const int8_t* position,
+                       const uint32_t* const* cols, int ld, int n_threads, uint32_t* y, uint32_t* N, uint32_t* mm) {
+  constexpr int kPos = 30, kMM = 12;
+  if (n < 0 || n_cat < 0 || ld < kPos || (n > 0 && (!codes || !position || !cols || !y || !N || !mm)))
+    return arg_error("mdi_pack_dense: bad arguments");
+  for (int c = 0; c < kMM + 4; ++c)
+    if (n > 0 && !cols[c]) return arg_error("mdi_pack_dense: bad column");
+  if (n % kPos) return MDI_E_LAYOUT;
+  const int64_t T = n / kPos;
+  // one pass over the blocks: write them, and check the layout on the way
+  // (a failed check returns MDI_E_LAYOUT; the caller's general path rewrites everything)
+  const int nt = pool_size(n_threads, n);
+  std::vector<uint8_t> bad((size_t)nt, 0);
+  for_ranges(nt, T, [&](int tid, int64_t lo, int64_t hi) {
+    bool b = false;
+    for (int64_t t = lo; t < hi; ++t) {
+      const int64_t r0 = t * kPos;
+      const int32_t k = codes[r0];
+      b |= k < 0 || k >= n_cat;
+      uint32_t* yt = y + t * ld;
+      uint32_t* Nt = N + t * ld;
+      for (int j = 0; j < kPos; ++j) {
+        const int64_t r = r0 + j;
+        const int want = j < 15 ? j + 1 : 14 - j;  // z = 1..15, -1..-15
+        b |= codes[r] != k || position[r] != want;
+        const int s = j < 15 ? 0 : 1;
+        yt[j] = cols[kMM + s][r];
+        Nt[j] = cols[kMM + 2 + s][r];
+        uint32_t* m = mm + r * kMM;
+        for (int c = 0; c < kMM; ++c) m[c] = cols[c][r];
+      }
+      for (int j = kPos; j < ld; ++j) yt[j] = Nt[j] = 0;
+    }
+    bad[(size_t)tid] = b;
+  });
+  for (int i = 0; i < nt; ++i)
+    if (bad[(size_t)i]) return MDI_E_LAYOUT;
+  // no tax_id code in two blocks (each taxon's rows contiguous)
+  std::vector<uint8_t> seen((size_t)n_cat, 0);
+  for (int64_t t = 0; t < T; ++t) {
+    uint8_t& s = seen[(size_t)codes[t * kPos]];
+    if (s) return MDI_E_LAYOUT;
+    s = 1;
+  }
+  return T;
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------

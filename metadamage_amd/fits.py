@@ -128,8 +128,41 @@ def pack_counts(df: pd.DataFrame, cfg, pinned: bool = False) -> Packed:
     if missing.any():
         df = df[~missing]
         tax = df["tax_id"]
-    # taxon index in first-appearance order (pd.factorize) and each taxon's first row
     codes = tax.cat.codes.to_numpy() if isinstance(tax.dtype, pd.CategoricalDtype) else None
+
+    def packed(first, y, N, mm, pp):
+        return Packed(
+            tax_id=_first_values(tax, first),
+            tax_name=_first_values(df["tax_name"], first),
+            tax_rank=_first_values(df["tax_rank"], first),
+            N_alignments=df["N_alignments"].to_numpy()[first].astype(np.int64),
+            y=y,
+            N=N,
+            mm=mm,
+            cats=_first_categoricals(df, first),
+            pinned=pp,
+        )
+
+    # the usual table (counts.compute_counts: 30 rows per taxon in z order,
+    # uint32 counts): one native pass writes y, N and mm and checks the layout
+    pos = df["position"].to_numpy()
+    n = len(tax)
+    if codes is not None and n and n % _lib.NPOS == 0 and pos.dtype == np.int8 and len(tax.cat.categories) < 2**31:
+        cols = [df[c].to_numpy() for c in (*MM_COLUMNS, fwd, rev, fwd[0], rev[0])]
+        if all(c.dtype == np.uint32 for c in cols):
+            from . import ingest
+
+            T = n // _lib.NPOS
+            y, N, mm, pp = _pack_buffers(T, pinned, zero=False)
+            T = ingest.pack_dense(np.ascontiguousarray(codes, dtype=np.int32), len(tax.cat.categories), pos,
+                                  [np.ascontiguousarray(c) for c in cols], y, N, mm)
+            if T >= 0:
+                return packed(np.arange(T, dtype=np.int64) * _lib.NPOS, y, N, mm, pp)
+            if pp is not None:
+                from . import engine
+
+                engine.release_pinned_pack(pp)
+    # taxon index in first-appearance order (pd.factorize) and each taxon's first row
     if codes is not None and len(tax.cat.categories) < 2**31:
         from . import ingest
 
@@ -140,7 +173,6 @@ def pack_counts(df: pd.DataFrame, cfg, pinned: bool = False) -> Packed:
         first = np.flatnonzero(np.r_[True, t[1:] > np.maximum.accumulate(t[:-1])]) if t.size else np.zeros(0, np.int64)
     n = t.size
     T = first.size
-    pos = df["position"].to_numpy()
     pos_fwd = pos > 0
     yv = _as_u32(np.where(pos_fwd, df[fwd].to_numpy(), df[rev].to_numpy()))
     Nv = _as_u32(np.where(pos_fwd, df[fwd[0]].to_numpy(), df[rev[0]].to_numpy()))
@@ -148,19 +180,7 @@ def pack_counts(df: pd.DataFrame, cfg, pinned: bool = False) -> Packed:
     dense = n == T * _lib.NPOS and np.array_equal(
         pos.reshape(T, _lib.NPOS), np.broadcast_to(POSITIONS.astype(pos.dtype), (T, _lib.NPOS))) and np.array_equal(
         t.reshape(T, _lib.NPOS), np.broadcast_to(np.arange(T)[:, None], (T, _lib.NPOS)))
-    pp = None
-    if pinned and T > 0:  # straight into a pinned buffer set (pinned=True: main.main's reader threads)
-        from . import engine
-
-        pp = engine.acquire_pinned_pack(T)
-    if pp is not None:
-        y, N, mm = pp.views(T)
-        y.fill(0)
-        N.fill(0)
-    else:
-        y = np.zeros((T, _lib.LD), np.uint32)
-        N = np.zeros((T, _lib.LD), np.uint32)
-        mm = np.empty((T, _lib.NPOS, _lib.NMM), np.uint32)
+    y, N, mm, pp = _pack_buffers(T, pinned, zero=True)
     if dense:
         y[:, :_lib.NPOS] = yv.reshape(T, _lib.NPOS)
         N[:, :_lib.NPOS] = Nv.reshape(T, _lib.NPOS)
@@ -177,17 +197,29 @@ def pack_counts(df: pd.DataFrame, cfg, pinned: bool = False) -> Packed:
         rows = np.empty((n, _lib.NMM), np.uint32)
         _interleave(mm_cols, rows)
         mm.reshape(-1, _lib.NMM)[(t * _lib.NPOS + col)[ok]] = rows[ok]
-    return Packed(
-        tax_id=_first_values(tax, first),
-        tax_name=_first_values(df["tax_name"], first),
-        tax_rank=_first_values(df["tax_rank"], first),
-        N_alignments=df["N_alignments"].to_numpy()[first].astype(np.int64),
-        y=y,
-        N=N,
-        mm=mm,
-        cats=_first_categoricals(df, first),
-        pinned=pp,
-    )
+    return packed(first, y, N, mm, pp)
+
+
+def _pack_buffers(T: int, pinned: bool, zero: bool):
+    """y, N (uint32[T][LD]) and mm (uint32[T][30][12]) for pack_counts, in a
+    pinned buffer set when pinned (main.main's reader threads: the device copy
+    reads them directly); zero: y and N zero-filled."""
+    pp = None
+    if pinned and T > 0:
+        from . import engine
+
+        pp = engine.acquire_pinned_pack(T)
+    if pp is not None:
+        y, N, mm = pp.views(T)
+        if zero:
+            y.fill(0)
+            N.fill(0)
+    else:
+        alloc = np.zeros if zero else np.empty
+        y = alloc((T, _lib.LD), np.uint32)
+        N = alloc((T, _lib.LD), np.uint32)
+        mm = np.empty((T, _lib.NPOS, _lib.NMM), np.uint32)
+    return y, N, mm, pp
 
 
 # --------------------------------------------------------------------------
@@ -391,9 +423,12 @@ def extract_top_max_fits(df_counts, max_fits):
     tax = df_counts["tax_id"]
     if isinstance(tax.dtype, pd.CategoricalDtype) and len(df_counts):
         codes = tax.cat.codes.to_numpy()
-        if codes.min() >= 0:
-            n_cat = len(tax.cat.categories)
-            present = np.flatnonzero(np.bincount(codes, minlength=n_cat))
+        n_cat = len(tax.cat.categories)
+        from . import ingest
+
+        used, n_missing = ingest.used_codes(codes, n_cat) if n_cat < 2**31 else (None, 1)
+        if n_missing == 0:
+            present = np.flatnonzero(used)
             if max_fits >= len(present):
                 return df_counts
             sums = np.bincount(codes, weights=df_counts["N_alignments"].to_numpy(np.float64), minlength=n_cat)

@@ -69,6 +69,10 @@ def _load():
         lib.mdi_first_index.restype = i64
         lib.mdi_interleave.argtypes = [i64, ctypes.c_int, vp, vp, ctypes.c_int]
         lib.mdi_interleave.restype = ctypes.c_int
+        lib.mdi_pack_dense.argtypes = [i64, vp, ctypes.c_int32, vp, vp, ctypes.c_int, ctypes.c_int, vp, vp, vp]
+        lib.mdi_pack_dense.restype = i64
+        lib.mdi_used_codes.argtypes = [i64, vp, ctypes.c_int32, ctypes.c_int, vp, vp]
+        lib.mdi_used_codes.restype = i64
         _LIB = lib
     return _LIB
 
@@ -84,6 +88,45 @@ def first_index(codes: np.ndarray, n_cat: int):
     if T < 0:
         raise ValueError(_load().mdi_counts_error().decode())
     return taxon, first[:T]
+
+
+MDI_E_LAYOUT = -5
+
+
+def used_codes(codes: np.ndarray, n_cat: int, n_threads: int = 0):
+    """(used bool[n_cat], n_missing) of a categorical's codes (mdi_used_codes):
+    which categories occur, and how many values are missing (code -1)."""
+    codes = np.ascontiguousarray(codes, dtype=np.int32)
+    used = np.empty(max(1, n_cat), np.uint8)
+    miss = ctypes.c_int64(0)
+    lib = _load()
+    if lib.mdi_used_codes(codes.size, codes.ctypes.data, int(n_cat), int(n_threads), used.ctypes.data,
+                          ctypes.byref(miss)) < 0:
+        raise ValueError(lib.mdi_counts_error().decode())
+    return used[:n_cat].view(bool), int(miss.value)
+
+
+def pack_dense(codes: np.ndarray, n_cat: int, position: np.ndarray, cols, y: np.ndarray, N: np.ndarray,
+               mm: np.ndarray, n_threads: int = 0) -> int:
+    """fits.pack_counts of the usual table in one native pass (mdi_pack_dense):
+    codes int32[30 T] (one tax_id code per 30-row block), position int8, cols =
+    16 uint32 columns (12 mismatch, y fwd / rev, N fwd / rev); fills y, N
+    (uint32[T][ld]) and mm (uint32[T][30][12]).  Returns T, or -1 when the
+    table is not in that layout (the outputs are then partly written)."""
+    n = codes.size
+    assert codes.dtype == np.int32 and position.dtype == np.int8 and len(cols) == 16
+    assert all(c.dtype == np.uint32 and c.size == n and c.flags.c_contiguous for c in cols)
+    T = n // 30
+    assert y.shape[0] >= T and N.shape == y.shape and mm.size >= T * 360 and y.flags.c_contiguous
+    assert N.flags.c_contiguous and mm.flags.c_contiguous and y.dtype == N.dtype == mm.dtype == np.uint32
+    lib = _load()
+    r = lib.mdi_pack_dense(n, codes.ctypes.data, int(n_cat), position.ctypes.data, _ptrs(cols, ctypes.c_void_p),
+                           int(y.shape[1]), int(n_threads), y.ctypes.data, N.ctypes.data, mm.ctypes.data)
+    if r == MDI_E_LAYOUT:
+        return -1
+    if r < 0:
+        raise ValueError(lib.mdi_counts_error().decode())
+    return int(r)
 
 
 def interleave(cols, out2d: np.ndarray, n_threads: int = 0) -> None:

@@ -109,8 +109,17 @@ class Config:
         return Path(self.out_dir) / "fit_predictions" / f"{self.shortname}.parquet"
 
     def set_number_of_fits(self, df_counts):
-        """utils.py:121-130."""
-        self.N_tax_ids = len(pd.unique(df_counts.tax_id))
+        """utils.py:121-130.  The distinct tax_ids (a missing value counts as
+        one, as in pd.unique) of a categorical column by one native pass over
+        its codes (ingest.used_codes)."""
+        tax = df_counts.tax_id
+        if isinstance(tax.dtype, pd.CategoricalDtype) and len(tax.cat.categories) < 2**31:
+            from . import ingest
+
+            used, n_missing = ingest.used_codes(tax.cat.codes.to_numpy(), len(tax.cat.categories))
+            self.N_tax_ids = int(used.sum()) + (n_missing > 0)
+        else:
+            self.N_tax_ids = len(pd.unique(tax))
         if self.max_fits is not None and self.max_fits > 0:
             self.N_fits = min(self.max_fits, self.N_tax_ids)
         else:

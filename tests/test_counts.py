@@ -7,7 +7,7 @@ import numpy as np
 import pandas as pd
 import pytest
 
-from metadamage_amd import counts, fits, utils
+from metadamage_amd import counts, fits, ingest, utils
 from tests.helpers import GOLDEN, MM_COLUMNS
 
 CASES = {
@@ -58,6 +58,43 @@ def test_packing_matches_group_to_numpyro_data(name, ref_meta, ref_golden):
     assert (p.y[:, 30:] == 0).all() and (p.N[:, 30:] == 0).all()
     mm = df[MM_COLUMNS].to_numpy().reshape(-1, 30, 12)
     assert (p.mm == mm).all()
+
+
+def _general_pack(df, cfg):
+    """pack_counts through its general path (an int16 position column skips
+    the native dense pass)."""
+    d = df.copy()
+    d["position"] = d["position"].astype(np.int16)
+    return fits.pack_counts(d, cfg)
+
+
+def _same_pack(a, b):
+    assert a.n_taxa == b.n_taxa
+    assert (a.y == b.y).all() and (a.N == b.N).all() and (a.mm == b.mm).all()
+    assert [str(x) for x in a.tax_id] == [str(x) for x in b.tax_id]
+    assert (a.N_alignments == b.N_alignments).all()
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_native_dense_pack_equals_general_path(name, ref_meta):
+    """ingest.pack_dense (mdi_pack_dense) packs the usual table exactly as the
+    general path; tables out of that layout (a taxon short of a row, a taxon
+    split in two blocks, positions out of z order) fall back to it."""
+    cfg = cfg_for(ref_meta["cases"][name], GOLDEN / CASES[name])
+    df = counts.compute_counts(cfg)
+    assert df["position"].dtype == np.int8 and df["AC"].dtype == np.uint32
+    _same_pack(fits.pack_counts(df, cfg), _general_pack(df, cfg))
+    if len(df) < 90:
+        return
+    short = df.drop(index=df.index[5]).reset_index(drop=True)  # ragged: 29 rows for the first taxon
+    _same_pack(fits.pack_counts(short, cfg), _general_pack(short, cfg))
+    split = pd.concat([df.iloc[:15], df.iloc[30:60], df.iloc[15:30], df.iloc[60:]]).reset_index(drop=True)
+    _same_pack(fits.pack_counts(split, cfg), _general_pack(split, cfg))
+    swapped = df.copy()
+    p = swapped["position"].to_numpy().copy()
+    p[[0, 1]] = p[[1, 0]]
+    swapped["position"] = p
+    _same_pack(fits.pack_counts(swapped, cfg), _general_pack(swapped, cfg))
 
 
 def test_packing_categorical_with_a_missing_tax_id(ref_meta):
@@ -386,3 +423,24 @@ def test_native_noise_matches_the_reference_restatement():
     assert np.array_equal(np.isnan(nz), np.isnan(ref))
     ok = ~np.isnan(ref)
     assert (np.abs(nz[ok] - ref[ok]) <= 1e-13 * np.abs(ref[ok])).all()
+
+
+@pytest.mark.parametrize("n_cat,missing", [(5, False), (5, True), (40_000, False), (40_000, True)])
+def test_number_of_fits_counts_distinct_tax_ids_like_pd_unique(n_cat, missing):
+    """utils.Config.set_number_of_fits on a categorical tax_id (native
+    ingest.used_codes) counts the distinct values as len(pd.unique(...)): unused
+    categories left out, a missing value counted once."""
+    rng = np.random.default_rng(n_cat)
+    vals = rng.choice(n_cat, size=3 * n_cat, replace=True)
+    cat = pd.Categorical(vals, categories=np.arange(n_cat + 3))
+    if missing:
+        cat[[1, 7]] = np.nan
+    df = pd.DataFrame({"tax_id": cat})
+    cfg = utils.Config(out_dir="/tmp/mdfit_unused", max_fits=None, max_cores=1, min_alignments=10, min_y_sum=10,
+                       substitution_bases_forward="CT", substitution_bases_reverse="GA", forced=False,
+                       version="0.0.0")
+    cfg.set_number_of_fits(df)
+    assert cfg.N_tax_ids == len(pd.unique(df.tax_id))
+    used, n_missing = ingest.used_codes(cat.codes, n_cat + 3)
+    assert n_missing == (2 if missing else 0)
+    assert (np.flatnonzero(used) == np.unique(cat.codes[cat.codes >= 0])).all()

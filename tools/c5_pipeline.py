@@ -63,28 +63,35 @@ def stages(files, out_dir, inference):
         cfg = _cfg(out_dir, inference)
         cfg.add_filename(f)
         t = {"file": f.name}
+        c = time.process_time()
         s = time.perf_counter()
         df = counts.compute_counts(cfg)
         t["ingest_s"] = time.perf_counter() - s
+        t["ingest_cpu"], c = time.process_time() - c, time.process_time()
         s = time.perf_counter()
         io.Parquet(cfg.filename_counts).save(df, metadata=cfg.to_dict())
         t["counts_parquet_s"] = time.perf_counter() - s
+        t["counts_parquet_cpu"], c = time.process_time() - c, time.process_time()
         s = time.perf_counter()
         p = fits.pack_counts(df, cfg)
         t["pack_s"] = time.perf_counter() - s
+        t["pack_cpu"], c = time.process_time() - c, time.process_time()
         s = time.perf_counter()
         out, pred, st = fits.fit_packed(p, fits.make_opts(cfg), shard=False)
         torch.cuda.synchronize()
         t["fit_s"] = time.perf_counter() - s
+        t["fit_cpu"], c = time.process_time() - c, time.process_time()
         s = time.perf_counter()
         keep = st == 0
         dfr = fits.make_df_fit_results(p, out, keep, cfg)
         dfp = fits.make_df_fit_predictions(p, pred, keep, cfg)
         t["frames_s"] = time.perf_counter() - s
+        t["frames_cpu"], c = time.process_time() - c, time.process_time()
         s = time.perf_counter()
         io.Parquet(cfg.filename_fit_results).save(dfr, metadata=cfg.to_dict())
         io.Parquet(cfg.filename_fit_predictions).save(dfp, metadata=cfg.to_dict())
         t["results_parquet_s"] = time.perf_counter() - s
+        t["results_parquet_cpu"] = time.process_time() - c
         t["taxa"] = int(p.n_taxa)
         print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in t.items()}), flush=True)
 
@@ -225,10 +232,12 @@ def main() -> None:
         dist.barrier()
     events = _trace_wrappers() if a.trace else None
     torch.cuda.synchronize()
+    c = time.process_time()
     s = time.perf_counter()
     res = driver.main(files, cfg)
     torch.cuda.synchronize()
     wall = time.perf_counter() - s
+    cpu = time.process_time() - c
     if events is not None and rank == 0:
         print(json.dumps({"trace": _trace_summary(events, s, wall)}), flush=True)
     taxa = sum(len(r[0]) for r in res.values() if r[0] is not None)
@@ -241,7 +250,8 @@ def main() -> None:
     if rank == 0:
         print(json.dumps({"config": "C5", "inference": a.inference, "files": a.files, "ranks": world,
                           "taxa_fitted": taxa, "wall_s": round(wall, 3), "taxa_per_s": round(taxa / wall, 1),
-                          "s_per_file": round(wall * world / a.files, 3)}), flush=True)
+                          "s_per_file": round(wall * world / a.files, 3),
+                          "process_cpu_s": round(cpu, 2)}), flush=True)
     if a.check:
         from metadamage_amd.utils import extract_name
 
