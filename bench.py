@@ -582,7 +582,7 @@ def host_to_host(engine, b, opts, dev, steps: int, generate=None) -> dict:
     out["unit"] = "fits/s"
     out["note"] = ("pinned host y,N (+mm) -> H2D -> fit -> D2H of the 32 record columns, predictions, status, "
                    "median of the calls, each synchronised; chunks > 1: ChunkedFitter's two streams overlap one "
-                   "chunk's copies with the other's fit (DESIGN.md 10); the PCIe-inclusive rate is never `value`")
+                   "chunk's copies with the other's fit (DESIGN.md 12); the PCIe-inclusive rate is never `value`")
     return out
 
 
