@@ -1397,7 +1397,14 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
   }
 
   // ---- waic_i per chain and point (fits.py:126-172), lanes over draws ----------
+  // (-DMDFIT_DEV_NOWAIC / -DMDFIT_DEV_NOPRED, development: the post kernel's
+  // split with one part compiled out -- never a product build)
+#ifdef MDFIT_DEV_NOWAIC
+  for (int x = lane; x < MDFIT_NSUBFIT * kNPos; x += kWave) (&s_waic[0][0])[x] = 1.0 + x;
+  for (int s = 0; s < 0; ++s) {
+#else
   for (int s = 0; s < MDFIT_NSUBFIT; ++s) {
+#endif
     const bool pmd = s == 0 || s == 2 || s == 3;
     const int lo = (s == 3 || s == 5) ? kNHalf : 0, hi = s < 2 ? kNPos : lo + kNHalf;
     for (int col = lo; col < hi; ++col) {
@@ -1499,8 +1506,13 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
     const int k = col < kNHalf ? col : col - kNHalf;
     const double nn = s_N[col];
     double m3[3];
+#ifdef MDFIT_DEV_NOPRED
+    if (true) {
+      m3[0] = m3[1] = m3[2] = nn;
+#else
     if (nn == 0.0) {
       m3[0] = m3[1] = m3[2] = NAN;
+#endif
     } else {
       const Stream st = make_stream(o.seed, o.index_base + t, s);
       bool bad = false;

@@ -28,6 +28,8 @@ def main() -> None:
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--mode", choices=["map", "nuts"], default="map")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--split", action="store_true",
+                    help="also the library's own event split (mdfit_profile_*): fit / chain kernel and the rest")
     a = ap.parse_args()
 
     import torch
@@ -58,6 +60,8 @@ def main() -> None:
             for _ in range(3 if a.mode == "map" else 1):
                 call()
             torch.cuda.synchronize()
+            if a.split:
+                lib.mdfit_profile_enable(1)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.steps):
@@ -65,6 +69,13 @@ def main() -> None:
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.steps
+            split = ""
+            if a.split:
+                ca, fk, nn = ctypes.c_double(), ctypes.c_double(), ctypes.c_int32()
+                lib.mdfit_profile_read(ctypes.byref(ca), ctypes.byref(fk), ctypes.byref(nn))
+                lib.mdfit_profile_enable(0)
+                if nn.value:
+                    split = f"  [kernel {fk.value / nn.value:.3f} ms, rest {(ca.value - fk.value) / nn.value:.3f} ms]"
             full = res.out.cpu().numpy()
             out = full[:, :25]
             st = res.status.cpu().numpy()
@@ -78,7 +89,7 @@ def main() -> None:
             evals = full[:, _lib.F_DIAG + 5::8][:, :6].sum() if a.mode == "map" else float("nan")
             print(f"rep {rep} {Path(path).name:24s} {ms:8.3f} ms  {a.taxa / ms * 1e3 / 1e6:6.2f} M fits/s  "
                   f"ok {np.mean(st == 0):.4f}  max rel dev vs first {dev:.1e} ({ndiff} taxa)  pred identical {same_pred}  "
-                  f"evals {evals:.0f}",
+                  f"evals {evals:.0f}{split}",
                   flush=True)
 
 
