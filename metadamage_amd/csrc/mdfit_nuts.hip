@@ -119,14 +119,8 @@ __device__ __forceinline__ double uniform(const Stream& s, uint32_t w2, uint32_t
   return u53(o.x, o.y);
 }
 
-// not inlined: its log / cos / sqrt temporaries then stay out of the chain
-// loop's register allocation (fewer spills on the hot path; measured -4 % C3
-// together with the momentum cache)
-__device__ __noinline__ double normal(const Stream& s, uint32_t w2, uint32_t w3) {
-  const uint4 o = block(s, w2, w3);
-  const double u1 = 1.0 - u53(o.x, o.y), u2 = u53(o.z, o.w);
-  return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
-}
+// (not inlined: their log / sincos / sqrt temporaries then stay out of the chain
+// loop's register allocation -- fewer spills on the hot path)
 // normal k of the Box-Muller pair of one block (k = 0: cos, 1: sin; oracle:
 // nnormal_k) -- the chain's momenta (draw convention 2)
 __device__ __noinline__ double normal_k(const Stream& s, uint32_t w2, uint32_t w3, int k) {
@@ -153,18 +147,24 @@ __device__ __noinline__ double2 normal_pair(const Stream& s, uint32_t w2, uint32
 #ifndef MDFIT_POST_FAST
 #define MDFIT_POST_FAST 1
 #endif
+// (MDFIT_WAIC_GROUP) the null sub-fits' WAIC takes G columns per pass over the
+// draws: a, b and a + b do not depend on the column there (D = q), so their
+// three lnGamma values are formed once per draw for G columns -- the same
+// values in the same expression, bit for bit (0: one column per pass)
+#ifndef MDFIT_WAIC_GROUP
+#define MDFIT_WAIC_GROUP 3
+#endif
+// the post kernel's occupancy floor (waves per SIMD; LDS allows ~6): 5 leaves
+// the grouped WAIC 96 VGPRs (26 spilled); at 6 it spills 44 and runs slower,
+// unbounded it takes 118 (4 waves), also slower (profiles/r06_ab_waic.txt)
+#ifndef MDFIT_POST_WAVES
+#define MDFIT_POST_WAVES 5
+#endif
 #ifndef MDFIT_NUTS_SST
 #define MDFIT_NUTS_SST 1
 #endif
 __device__ __forceinline__ double pexp(double x) { return MDFIT_POST_FAST ? fexp_t(x) : exp(x); }
 __device__ __forceinline__ double plog(double x) { return MDFIT_POST_FAST ? flog_t<true>(x) : log(x); }
-
-// the same, inlined (the post kernel's draws: no call per normal)
-__device__ __forceinline__ double normal_inl(const Stream& s, uint32_t w2, uint32_t w3) {
-  const uint4 o = block(s, w2, w3);
-  const double u1 = 1.0 - u53(o.x, o.y), u2 = u53(o.z, o.w);
-  return sqrt(-2.0 * plog(u1)) * cos(6.283185307179586 * u2);
-}
 
 __device__ __forceinline__ bool active(bool pmd, int j) { return pmd || j == 0 || j == 3; }
 
@@ -1190,11 +1190,38 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_NUT
 // post kernel: one wave per taxon
 // ---------------------------------------------------------------------------
 // frac = obs / N of one predictive Beta-Binomial draw (oracle: predictive_frac)
+// (predictive draw convention 2, round 6: a block gives two uniforms -- words
+// 0-1, then 2-3 -- or a Box-Muller pair of normals -- cos, then sin; the two
+// kinds take blocks from one counter in the order they run dry; oracle: ndraw)
 struct Draw {
   const Stream* st;
   uint32_t w2, w3;
-  __device__ double uni() { return uniform(*st, w2, w3++); }
-  __device__ double nrm() { return normal_inl(*st, w2, w3++); }
+  double uc = 0.0, nc = 0.0;  // the block's second uniform / normal
+  bool uh = false, nh = false;
+  __device__ double uni() {
+    if (uh) {
+      uh = false;
+      return uc;
+    }
+    const uint4 o = block(*st, w2, w3++);
+    uc = u53(o.z, o.w);
+    uh = true;
+    return u53(o.x, o.y);
+  }
+  __device__ double nrm() {
+    if (nh) {
+      nh = false;
+      return nc;
+    }
+    const uint4 o = block(*st, w2, w3++);
+    const double u1 = 1.0 - u53(o.x, o.y), u2 = u53(o.z, o.w);
+    double sn, cs;
+    sincos(6.283185307179586 * u2, &sn, &cs);
+    const double r = sqrt(-2.0 * plog(u1));
+    nc = r * sn;
+    nh = true;
+    return r * cs;
+  }
 };
 
 __device__ double log_gamma_draw(Draw& d, double alpha) {
@@ -1335,7 +1362,64 @@ __device__ void median_hpdi_counts(const uint32_t* c, int S, double Nn, double o
   out3[2] = f(best + len);
 }
 
-__global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __restrict__ gy,
+#if MDFIT_WAIC_GROUP > 1
+// waic_i (fits.py:126-172) of G columns whose draws share D (so a, b, a + b):
+// one pass over the draws, their three lnGamma values formed once per draw;
+// per column the same expression and accumulators as the one-column pass
+template <int G>
+__device__ __forceinline__ void waic_cols(int lane, int S, const double* smp, bool pmd, int k, const int* cols,
+                                          const double* s_y, const double* s_N, double* waic_row) {
+#pragma clang fp contract(off)
+  double lc[G], mxl[G], sel[G], mul[G], m2l[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const double yy = s_y[cols[g]], nn = s_N[cols[g]];
+    lc[g] = lg3<false, MDFIT_TLOG_NUTS>(nn + 1.0).l - lg3<false, MDFIT_TLOG_NUTS>(yy + 1.0).l -
+            lg3<false, MDFIT_TLOG_NUTS>(nn - yy + 1.0).l;
+    mxl[g] = -INFINITY;
+    sel[g] = mul[g] = m2l[g] = 0.0;
+  }
+  double cnt = 0.0;
+  for (int x = lane; x < S; x += kWave) {
+    const double* th = smp + (int64_t)x * 4;
+    const double D = d_at(th, pmd, k), phi = th[3];
+    const double a = D * phi, b = (1.0 - D) * phi;
+    const double la = lg3<false, MDFIT_TLOG_NUTS>(a).l, lb = lg3<false, MDFIT_TLOG_NUTS>(b).l,
+                 lab = lg3<false, MDFIT_TLOG_NUTS>(a + b).l;
+    cnt += 1.0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const double yy = s_y[cols[g]], nn = s_N[cols[g]];  // (LDS broadcasts: no registers held)
+      const double lp = lc[g] + (lg3<false, MDFIT_TLOG_NUTS>(yy + a).l - la) +
+                        (lg3<false, MDFIT_TLOG_NUTS>(nn - yy + b).l - lb) -
+                        (lg3<false, MDFIT_TLOG_NUTS>(nn + phi).l - lab);
+      if (lp == -INFINITY) {
+      } else if (lp > mxl[g]) {
+        sel[g] = sel[g] * pexp(mxl[g] - lp) + 1.0;
+        mxl[g] = lp;
+      } else {
+        sel[g] += pexp(lp - mxl[g]);
+      }
+      const double dlt = lp - mul[g];
+      mul[g] += dlt / cnt;
+      m2l[g] = fma(dlt, lp - mul[g], m2l[g]);
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const double mx = wmax(mxl[g]);
+    const double se = wsum(cnt > 0.0 ? sel[g] * pexp(mxl[g] - mx) : 0.0);
+    const double mean = wsum(cnt * mul[g]) / S;
+    const double dm = mul[g] - mean;
+    const double var = wsum(m2l[g] + cnt * dm * dm) / S;
+    const double lppd = mx + log(se) - log((double)S);
+    if (lane == 0) waic_row[cols[g]] = -2.0 * (lppd - var);
+  }
+  __syncthreads();
+}
+#endif
+
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_POST_WAVES))) void nuts_post_kernel(const uint32_t* __restrict__ gy,
                                                           const uint32_t* __restrict__ gN,
                                                           const uint32_t* __restrict__ gmm, int64_t n_taxa,
                                                           mdfit_opts o, const double* __restrict__ samples,
@@ -1405,8 +1489,32 @@ __global__ __launch_bounds__(kWave) void nuts_post_kernel(const uint32_t* __rest
 #else
   for (int s = 0; s < MDFIT_NSUBFIT; ++s) {
 #endif
+    // (no contraction: the grouped and the per-column passes then round every
+    // lp alike -- fusing D * phi into yy + a depends on how often a is used)
+#pragma clang fp contract(off)
     const bool pmd = s == 0 || s == 2 || s == 3;
     const int lo = (s == 3 || s == 5) ? kNHalf : 0, hi = s < 2 ? kNPos : lo + kNHalf;
+#if MDFIT_WAIC_GROUP > 1
+    // columns sharing D share a, b and a + b: every column of a null sub-fit
+    // (D = q; groups of MDFIT_WAIC_GROUP), and in the PMD all-position sub-fit
+    // the pair z = k+1 / -(k+1) (one k)
+    if (!pmd) {
+      for (int c0 = lo; c0 < hi; c0 += MDFIT_WAIC_GROUP) {
+        int cols[MDFIT_WAIC_GROUP];
+#pragma unroll
+        for (int g = 0; g < MDFIT_WAIC_GROUP; ++g) cols[g] = c0 + g;
+        waic_cols<MDFIT_WAIC_GROUP>(lane, S, smp + (int64_t)s * S * 4, false, 0, cols, s_y, s_N, s_waic[s]);
+      }
+      continue;
+    }
+    if (s == 0) {
+      for (int k = 0; k < kNHalf; ++k) {
+        const int cols[2] = {k, kNHalf + k};
+        waic_cols<2>(lane, S, smp, true, k, cols, s_y, s_N, s_waic[0]);
+      }
+      continue;
+    }
+#endif
     for (int col = lo; col < hi; ++col) {
       const double yy = s_y[col], nn = s_N[col];
       const int k = col < kNHalf ? col : col - kNHalf;

@@ -56,7 +56,9 @@
  *                         2m (words 0-1) and 2m + 1 (words 2-3)
  *   init attempt a:       word2 = 0xFFFF0000 + a, word3 = dim
  *   step-size search f,m: word2 = 0xFFFE0000 + 4096 f + m, word3 = dim
- *   predictive draw s, i: word2 = 0xFFFD0000 + s, word3 = (i << 16) + k
+ *   predictive draw s, i: word2 = 0xFFFD0000 + s, word3 = (i << 16) + k, the
+ *                         k-th block of the draw: two uniforms or two normals
+ *                         (predictive draw convention 2, round 6)
  */
 
 #define NUTS_MAX_DEPTH 10
@@ -117,14 +119,6 @@ static double nuniform(const nstream* s, uint32_t w2, uint32_t w3) {
   uint32_t o[4];
   nblock(s, w2, w3, o);
   return u53(o[0], o[1]);
-}
-
-static double nnormal(const nstream* s, uint32_t w2, uint32_t w3) {
-  uint32_t o[4];
-  nblock(s, w2, w3, o);
-  const double u1 = 1.0 - u53(o[0], o[1]); /* (0, 1] */
-  const double u2 = u53(o[2], o[3]);
-  return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
 }
 
 /* the Box-Muller pair of one block: cos (k = 0) or sin (k = 1) */
@@ -561,10 +555,37 @@ static void nuts_chain(const nctx* cx, const nstream* st, int nwarm, int nsamp, 
 typedef struct {
   const nstream* st;
   uint32_t w2, w3;
+  double uc, nc; /* the current block's second uniform / normal */
+  int uh, nh;
 } ndraw; /* sequential draws of one variate */
 
-static double dr_uniform(ndraw* d) { return nuniform(d->st, d->w2, d->w3++); }
-static double dr_normal(ndraw* d) { return nnormal(d->st, d->w2, d->w3++); }
+/* predictive draw convention 2 (round 6): a block gives two uniforms (words
+ * 0-1, then 2-3) or a Box-Muller pair of normals (cos, then sin); the two
+ * kinds take blocks from one counter in the order they run dry */
+static double dr_uniform(ndraw* d) {
+  if (d->uh) {
+    d->uh = 0;
+    return d->uc;
+  }
+  uint32_t o[4];
+  nblock(d->st, d->w2, d->w3++, o);
+  d->uc = u53(o[2], o[3]);
+  d->uh = 1;
+  return u53(o[0], o[1]);
+}
+static double dr_normal(ndraw* d) {
+  if (d->nh) {
+    d->nh = 0;
+    return d->nc;
+  }
+  uint32_t o[4];
+  nblock(d->st, d->w2, d->w3++, o);
+  const double u1 = 1.0 - u53(o[0], o[1]), u2 = u53(o[2], o[3]);
+  const double r = sqrt(-2.0 * log(u1)), a = 6.283185307179586 * u2;
+  d->nc = r * sin(a);
+  d->nh = 1;
+  return r * cos(a);
+}
 
 /* log of a Gamma(alpha, 1) draw (Marsaglia & Tsang; alpha < 1 boosted by u^(1/alpha)) */
 static double log_gamma_draw(ndraw* d, double alpha) {
@@ -639,7 +660,7 @@ static double binomial_draw(ndraw* d, double n, double p) {
 static double predictive_frac(const nstream* st, int s, int i, int k, double Nn, const double th[4], int pmd) {
   double D = pmd ? th[1] * pow(1.0 - th[0], (double)k) + th[2] : th[0];
   D = D < 0.0 ? 0.0 : (D > 1.0 ? 1.0 : D);
-  ndraw d = {st, 0xFFFD0000u + (uint32_t)s, (uint32_t)i << 16};
+  ndraw d = {st, 0xFFFD0000u + (uint32_t)s, (uint32_t)i << 16, 0.0, 0.0, 0, 0};
   const double p = beta_draw(&d, D * th[3], (1.0 - D) * th[3]);
   const double obs = binomial_draw(&d, Nn, p);
   return obs / Nn; /* 0/0 -> NaN like numpy */

@@ -183,7 +183,11 @@ def test_predictive_draws_follow_the_beta_binomial(oracle_lib):
         D = A + c
         var = D * (1 - D) * (phi + N) / (N * (phi + 1))
         assert abs(frac.mean() - D) < 5 * np.sqrt(var / S)
-        assert abs(frac.var() / var - 1) < 0.1
+        # the sample variance's relative standard error from the sample's own
+        # kurtosis (the a = 0.01 case is heavy-tailed: ~0.14 at S = 20k)
+        dev = frac - frac.mean()
+        se = np.sqrt((np.mean(dev**4) / frac.var() ** 2 - 1.0) / S)
+        assert abs(frac.var() / var - 1) < max(0.1, 4 * se)
 
 
 def test_sharded_calls_draw_the_same_numbers(oracle_lib):
