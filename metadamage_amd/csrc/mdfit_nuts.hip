@@ -160,6 +160,11 @@ __device__ __noinline__ double2 normal_pair(const Stream& s, uint32_t w2, uint32
 #ifndef MDFIT_POST_WAVES
 #define MDFIT_POST_WAVES 5
 #endif
+// (MDFIT_REG_SORT) the predictive counts of 513..1024 draws sorted in
+// registers (reg_sort_u32); else the LDS bitonic sort
+#ifndef MDFIT_REG_SORT
+#define MDFIT_REG_SORT 1
+#endif
 #ifndef MDFIT_NUTS_SST
 #define MDFIT_NUTS_SST 1
 #endif
@@ -1333,6 +1338,56 @@ __device__ void lds_sort_u32(uint32_t* v, int n) {
     }
   }
 }
+// the same sort of n <= 64 R counts with the values in registers: lane L holds
+// elements 16 L .. 16 L + 15 (R = 16: n <= 1024, the reference's 1000 draws);
+// strides below R are compare-exchanges inside the lane, the others one
+// cross-lane exchange per value -- no LDS round trip and no barrier per stage.
+// The sorted sequence is the LDS sort's (a sort's result is unique).
+template <int R>
+__device__ void reg_sort_u32(uint32_t* v_lds, int n) {
+  const int lane = threadIdx.x;
+  uint32_t v[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int e = lane * R + j;
+    v[j] = e < n ? v_lds[e] : 0xFFFFFFFFu;
+  }
+#pragma unroll
+  for (int k = 2; k <= kWave * R; k <<= 1) {
+#pragma unroll
+    for (int s = k >> 1; s > 0; s >>= 1) {
+      if (s >= R) {
+        const int ls = s / R;
+        const bool upper = (lane & ls) != 0;
+        const bool asc = ((lane * R) & k) == 0;
+        const bool take_max = upper == asc;
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          const uint32_t p = (uint32_t)__shfl_xor((int)v[j], ls, kWave);
+          v[j] = take_max ? max(v[j], p) : min(v[j], p);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          if (j & s) continue;
+          const int jj = j | s;
+          const bool asc = k >= R ? (((lane * R) & k) == 0) : ((j & k) == 0);
+          const uint32_t a = v[j], b = v[jj];
+          const uint32_t lo = min(a, b), hi = max(a, b);
+          v[j] = asc ? lo : hi;
+          v[jj] = asc ? hi : lo;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int e = lane * R + j;
+    if (e < n) v_lds[e] = v[j];
+  }
+  __syncthreads();
+}
+
 // np.median + numpyro hpdi(prob 0.68) over the fractions c / N of the S sorted
 // counts c: each fraction is formed as the oracle's predictive_frac forms it,
 // so the result is its median_hpdi on the sorted fractions bit for bit
@@ -1633,7 +1688,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(MDFIT_POS
       if (__any(bad)) {  // (wave-uniform) the oracle: any NaN fraction -> NaN median and HPDI
         m3[0] = m3[1] = m3[2] = NAN;
       } else {
-        lds_sort_u32(s_c, S);
+#if MDFIT_REG_SORT
+        if (S > kWave * 8 && S <= kWave * 16)
+          reg_sort_u32<16>(s_c, S);
+        else
+#endif
+          lds_sort_u32(s_c, S);
         median_hpdi_counts(s_c, S, nn, m3);
       }
       __syncthreads();
