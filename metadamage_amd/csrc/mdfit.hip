@@ -1103,7 +1103,7 @@ __global__ __launch_bounds__(kWave) void noise_kernel(const uint32_t* __restrict
 // K4: 68 % predictive HPDI (MDFIT-HPDI v2, mdfit_hpdi.h) of the PMD-all mode at
 // every position (fits.py:112-120, 260-261).  K4a: one lane per (taxon,
 // position) -- neighbouring lanes hold neighbouring positions of one taxon;
-// windows of sd <= 100 points are finished there (the greedy), wide ones go to
+// windows of sd <= 40 points are finished there (the greedy), wide ones go to
 // a compacted list.  K4b: persistent; each lane runs one wide window's state
 // machine at a time and refills from the list (mdfit_hpdi.h).
 // Sources: the fit record (kFit: PMD-all (q, A, c, phi) + N; pred == nullptr

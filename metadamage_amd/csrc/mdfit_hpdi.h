@@ -8,7 +8,7 @@
 // reference `hp_greedy`): the pmf is unimodal for phi > 2, so the shortest 68 %
 // window grows from the mode by adding the more probable neighbour (a tie adds
 // the lower one) until it holds >= 0.68.  Same spec as the oracle's `hp_window`:
-//   * sd <= 100 points, or the mode alone holds 0.68: that greedy, one point per
+//   * sd <= 40 points (round 6; 100 before), or the mode alone holds 0.68: that greedy, one point per
 //     step through the ratio p(y+1)/p(y) -- `prep_position`, inline in K4a;
 //   * otherwise ("wide" windows) Newton on the level t of
 //     {y : ln p(y) >= ln p(m) + t} (or, when the window is clamped at 0 / N, on
@@ -58,7 +58,7 @@ __device__ unsigned long long g_hpdi_cnt[32];
 
 constexpr double kMass = 0.68;
 #ifndef MDFIT_HPDI_SIG_GREEDY
-#define MDFIT_HPDI_SIG_GREEDY 100.0
+#define MDFIT_HPDI_SIG_GREEDY 40.0
 #endif
 constexpr double kSigGreedy = MDFIT_HPDI_SIG_GREEDY;
 constexpr double kT0 = -0.49447329849;  // -Z68^2 / 2

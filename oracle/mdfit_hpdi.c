@@ -17,7 +17,7 @@
  * Two ways to the same window:
  *   hp_greedy  -- the definition, point by point (p(y+1) = p(y) R(y));
  *   hp_window  -- the spec the kernel implements: the greedy when the
- *                 predictive sd is <= 100 points (or the mode alone holds 68 %),
+ *                 predictive sd is <= 40 points (round 6; 100 before) (or the mode alone holds 68 %),
  *                 otherwise a Newton iteration on the level set
  *                 {y : ln p(y) >= ln p(m) + t} (two-sided), or on the window end
  *                 when the window is clamped at 0 or N (one-sided), with the
@@ -43,7 +43,7 @@
 
 #define HP_MASS 0.68
 #ifndef HP_SIG_GREEDY
-#define HP_SIG_GREEDY 100.0 /* sd (counts) up to which the greedy itself runs */
+#define HP_SIG_GREEDY 40.0 /* sd (counts) up to which the greedy itself runs (round 6: 100 before) */
 #endif
 #define HP_T0 (-0.49447329849) /* -Z68^2 / 2: the Gaussian 68 % level */
 #define HP_K0 16               /* exact sums this close to a support end */
