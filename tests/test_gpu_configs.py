@@ -1,8 +1,8 @@
 """GPU tests at the BASELINE.json configurations beyond the C2 bench size:
 
   * C4's per-GPU share (1M TaxIDs / 8 = 125k, seed 3): every taxon against the
-    CPU oracle (all result columns; the predictive HPDI on a sample -- the
-    oracle's long-double HPDI is the slow part of the checker);
+    CPU oracle, every result column and every predictive window (round 6: the
+    whole share; round 5 checked the HPDI on a 2,000-taxon sample);
   * C3 (100k TaxIDs, the reference's NUTS, seed 2): status and finiteness of
     every record, sampler streams keyed by the global taxon index (a slice
     refitted on its own with index_base reproduces the full run's records),
@@ -40,21 +40,19 @@ def test_c4_per_gpu_share_vs_oracle(engine, oracle_lib):
 
     b = generate(125_000, seed=3)
     out, pred, st = engine.fit_batch(b.y, b.N, b.mm)
-    ref_out, ref_pred, ref_st = oracle_lib.fit_batch(b.y, b.N, b.mm, hpdi=False)
+    ref_out, ref_pred, ref_st = oracle_lib.fit_batch(b.y, b.N, b.mm)
     # identical statuses for every taxon (the polish phase)
     assert (st == ref_st).all(), np.where(st != ref_st)[0][:10]
     both = st == 0
     assert both.all(), np.bincount(st)
-    cols = [j for j in range(25) if j not in HPDI_COLS]
-    rel = mixed_rel(out[both][:, cols], ref_out[both][:, cols])
+    rel = mixed_rel(out[both][:, :25], ref_out[both][:, :25])
     assert rel.max() < RTOL, (rel.max(), np.unravel_index(rel.argmax(), rel.shape))
     assert np.nanmax(mixed_rel(pred[both, 0], ref_pred[both, 0])) < 1e-5
-    # the predictive HPDI (D_max columns and every prediction bound) on a sample
-    idx = np.sort(np.random.default_rng(4).choice(b.n_taxa, 2000, replace=False))
-    s_out, s_pred, s_st = oracle_lib.fit_batch(b.y[idx], b.N[idx], b.mm[idx])
-    ok = (s_st == 0) & (st[idx] == 0)
-    assert mixed_rel(out[idx][ok][:, list(HPDI_COLS)], s_out[ok][:, list(HPDI_COLS)]).max() < RTOL
-    assert np.nanmax(mixed_rel(pred[idx][ok][:, 1:], s_pred[ok][:, 1:])) < RTOL
+    # every predictive window of the share (3.75M) within the result bar, and
+    # identical counts for all but a handful of near-ties
+    hp = mixed_rel(pred[both][:, 1:], ref_pred[both][:, 1:])
+    assert np.nanmax(hp) < RTOL, np.nanmax(hp)
+    assert (hp > 2e-5).sum() <= 10, (hp > 2e-5).sum()
 
 
 def test_c3_nuts_100k(engine, oracle_lib):
