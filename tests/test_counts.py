@@ -444,3 +444,15 @@ def test_number_of_fits_counts_distinct_tax_ids_like_pd_unique(n_cat, missing):
     used, n_missing = ingest.used_codes(cat.codes, n_cat + 3)
     assert n_missing == (2 if missing else 0)
     assert (np.flatnonzero(used) == np.unique(cat.codes[cat.codes >= 0])).all()
+
+
+@pytest.mark.parametrize("strings", [[], ["a"], ["", "x", ""], ["Escherichia coli", "Bacillus", "β-proteobacterium", "日本"],
+                                     [f"taxon {i} sp." for i in range(1000)]])
+def test_string_table_split_matches_per_string_decode(strings):
+    """ingest._split_strings (one decode and split) gives the string table the
+    per-string slices gave, empty and non-ASCII names included."""
+    enc = [s.encode() for s in strings]
+    raw = b"".join(enc) + b"\0"
+    off = np.concatenate([[0], np.cumsum([len(e) for e in enc])]).astype(np.int64)
+    got = ingest._split_strings(raw, off, len(strings))
+    assert got.dtype == object and list(got) == strings
