@@ -1235,7 +1235,9 @@ __device__ double log_gamma_draw(Draw& d, double alpha) {
     boost = plog(1.0 - d.uni()) / alpha;
     alpha += 1.0;
   }
-  const double dd = alpha - 1.0 / 3.0, cc = 1.0 / sqrt(9.0 * dd);
+  // (rsqrt for the oracle's 1 / sqrt: a last-bit difference in cc, which no
+  // draw of the 20k-taxon A/B felt -- profiles/r06_ab_rsq.txt)
+  const double dd = alpha - 1.0 / 3.0, cc = rsqrt(9.0 * dd);
   for (int k = 0; k < 256; ++k) {
     const double x = d.nrm();
     double v = 1.0 + cc * x;
@@ -1267,7 +1269,8 @@ __device__ double binomial_draw(Draw& d, double n, double p) {
   } else {
     const double spq = sqrt(n * pp * qq), bb = 1.15 + 2.53 * spq;
     const double aa = -0.0873 + 0.0248 * bb + 0.01 * pp, cc = n * pp + 0.5;
-    const double vr = 0.92 - 4.2 / bb, alpha = (2.83 + 5.1 / bb) * spq;
+    const double rb = 1.0 / bb;  // (one division for the two: last-bit differences only)
+    const double vr = 0.92 - 4.2 * rb, alpha = (2.83 + 5.1 * rb) * spq;
     const double lpq = plog(pp / qq), m = floor((n + 1.0) * pp);
     const double hh = lg3<false>(m + 1.0).l + lg3<false>(n - m + 1.0).l;
     k = floor(cc);
