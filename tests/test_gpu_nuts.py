@@ -88,6 +88,26 @@ def test_short_chains_follow_the_oracle_draw_for_draw(nuts_engine, oracle_lib):
     assert (dl > 1e-9).mean() <= 0.05, (dl > 1e-9).mean()
 
 
+def test_register_sort_path_follows_the_oracle(nuts_engine, oracle_lib):
+    """600 draws: the post kernel sorts the predictive counts in registers
+    (513..1024 draws; 100 take the LDS sort above).  Chains that match the
+    oracle draw for draw must give its records -- predictive medians, HPDI
+    bounds and WAIC columns -- to 1e-6."""
+    from metadamage_amd.synthetic import generate
+
+    b = generate(16, seed=5)
+    out, pred, st, smp = _run(nuts_engine, b, 1, 600, keep=True)
+    ro, rp, rs, rsmp = oracle_lib.nuts_batch(b.y, b.N, b.mm, num_warmup=1, num_samples=600, threads=8,
+                                             keep_samples=True)
+    assert (st == 0).all() and (rs == 0).all()
+    same = (np.abs(smp - rsmp).max(axis=(2, 3)) < 1e-6).all(1)
+    assert same.mean() >= 0.5, same.mean()
+    rel = np.abs(out[same, :25] - ro[same, :25]) / np.maximum(np.abs(ro[same, :25]), 1e-2)
+    assert np.nanmax(rel) < 1e-6, np.nanmax(rel, 0)
+    prel = np.abs(pred[same] - rp[same]) / np.maximum(np.abs(rp[same]), 1e-2)
+    assert np.nanmax(prel) < 1e-6, np.nanmax(prel)
+
+
 def _mcse(x, nb=20):
     m = x.shape[-1] // nb
     bm = x[..., : m * nb].reshape(x.shape[:-1] + (nb, m)).mean(-1)
