@@ -150,7 +150,7 @@ __device__ __noinline__ double2 normal_pair(const Stream& s, uint32_t w2, uint32
 // (MDFIT_WAIC_GROUP) the null sub-fits' WAIC takes G columns per pass over the
 // draws: a, b and a + b do not depend on the column there (D = q), so their
 // three lnGamma values are formed once per draw for G columns -- the same
-// values in the same expression, bit for bit (0: one column per pass)
+// values in the same expression, bit for bit (1: one column per pass)
 #ifndef MDFIT_WAIC_GROUP
 #define MDFIT_WAIC_GROUP 3
 #endif
